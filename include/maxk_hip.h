@@ -1,0 +1,144 @@
+/*
+ * maxk_hip.h -- C ABI of the MI355X-native MaxK-GNN aggregation hot path
+ * (libmaxk_hip.so, built from spgemm-prunning_amd/csrc for gfx950).
+ *
+ * Plain pointers and sizes only.  Every device pointer is caller-owned device
+ * memory; every launch goes on the caller's stream (a hipStream_t passed as
+ * void*; NULL = the default stream).  Launch functions never allocate, copy to
+ * the host or synchronise, so they can be captured into a hipGraph; the setup
+ * helpers marked "synchronous" do.
+ *
+ * Return value: MAXK_OK (0) or a negative MAXK_ERR_*; maxk_last_error() then
+ * holds a message for the calling thread.
+ *
+ * Layouts (all row-major, C-contiguous):
+ *   CSR     row_ptr int32 [num_rows+1], col_idx int32 [num_e] (< num_cols),
+ *           edge_val f32 [num_e]
+ *   CBSR    cbsr_val f32 [num_cols, k], cbsr_idx u8 [num_cols, k] (< dim_origin)
+ *   dense   f32 [rows, dim_origin]
+ *   warp4   int32 [W, 4] = (row, loc, len, 0)
+ * Limits: 1 <= k <= dim_origin <= 256 (the selector is uint8).
+ */
+#ifndef MAXK_HIP_H_
+#define MAXK_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAXK_OK 0
+#define MAXK_ERR_INVALID (-1)  /* bad argument (shape, null pointer, k/D range, workspace) */
+#define MAXK_ERR_HIP (-2)      /* a HIP runtime call or launch failed */
+#define MAXK_ERR_NODEVICE (-3) /* no HIP device visible */
+#define MAXK_ERR_LIBRARY (-4)  /* rocSPARSE failure (baseline only) */
+
+/* ABI version (major*100 + minor). */
+int maxk_version(void);
+
+/* Message for the last failing call on this thread ("" if none). */
+const char *maxk_last_error(void);
+
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int maxk_device_count(void);
+
+/* ---------------------------------------------------------------------------
+ * Forward row-wise-product SpGEMM:  out = diag(1/row_div) . A . scatter(cbsr)
+ *   out[r, cbsr_idx[c,l]] += edge_val[e] * cbsr_val[c,l]   (e in row r, c = col_idx[e])
+ * Every output row is written (rows without edges get zeros): no zero-init of
+ * `out` is needed.  row_div may be NULL (no normalisation).
+ * Replaces: spmm_kernel_opt2_sparse_v3 (kernels/spmm_maxk.cu:17-106),
+ *           its launcher spmm_kernel_opt2_sparse_v3_wrapper
+ *           (cuda_kernel_wrappers.cu:38-56) and the /in_degrees of
+ *           maxk_spgemm_function.py:85-86.
+ * chunk_edges: edges per wavefront work item (0 = auto).
+ * workspace: >= maxk_spgemm_forward_workspace_size(...) bytes (split-row slabs).
+ * ------------------------------------------------------------------------- */
+size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t num_e, int32_t dim_origin,
+                                          int32_t dim_k, int32_t chunk_edges);
+int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                        const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div,
+                        float *out, int64_t num_rows, int64_t num_cols, int64_t num_e,
+                        int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                        void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Backward outer-product sampled SpMM (SSpMM):
+ *   grad_cbsr[c,l] = sum_{e=(r->c)} edge_val[e] * grad_out[r, cbsr_idx[c,l]] / row_div[r]
+ *                  = (A^T diag(1/row_div) G)[c, cbsr_idx[c,l]]     (from the CSR of A)
+ * grad_cbsr [num_cols, k] is fully overwritten.  row_div may be NULL.
+ * Replaces: spmm_kernel_opt2_sparse_backward_v3 (kernels/spmm_maxk_backward.cu:15-115),
+ *           spmm_kernel_opt2_sparse_backward_v3_wrapper (cuda_kernel_wrappers.cu:58-76)
+ *           and the /out_degrees of maxk_spgemm_function.py:154-155.
+ * ------------------------------------------------------------------------- */
+size_t maxk_sspmm_backward_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                          int32_t dim_origin, int32_t dim_k, int32_t chunk_edges);
+int maxk_sspmm_backward(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                        const float *grad_out, const float *row_div, const uint8_t *cbsr_idx,
+                        float *grad_cbsr, int64_t num_rows, int64_t num_cols, int64_t num_e,
+                        int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                        void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * CBSR encode (MaxK top-k): per row the k largest of dim_origin values, in
+ * torch.topk(largest=True, sorted=True) order (value descending; NaN largest;
+ * equal values by ascending column).  x has leading dimension ld_x (elements).
+ * Replaces: torch.topk + .to(uint8) in maxk_spgemm_function.py:51-57 and the
+ *           uint8 kernel topk (kernels/maxk_kernel.cu:23-96) behind
+ *           cuda_topk_maxk / cuda_topk_maxk_float (cuda_kernel_bindings.cpp:164-238).
+ * maxk_topk_cbsr_u8: the same on uint8 input (values copied as uint8).
+ * idx32 (optional, may be NULL): the same indices widened to int32.
+ * ------------------------------------------------------------------------- */
+int maxk_topk_cbsr(const float *x, int64_t ld_x, float *cbsr_val, uint8_t *cbsr_idx,
+                   int32_t *idx32, int64_t num_rows, int32_t dim_origin, int32_t dim_k,
+                   void *stream);
+int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_val, uint8_t *cbsr_idx,
+                      int32_t *idx32, int64_t num_rows, int32_t dim_origin, int32_t dim_k,
+                      void *stream);
+
+/* dense[r,:] = 0; dense[r, cbsr_idx[r,l]] = cbsr_val[r,l]  (all of dense written).
+ * Replaces: zeros(V,D).scatter_(1, sel, grad_sparse), maxk_spgemm_function.py:152,175. */
+int maxk_cbsr_scatter_dense(const float *cbsr_val, const uint8_t *cbsr_idx, float *dense,
+                            int64_t num_rows, int32_t dim_origin, int32_t dim_k, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * warp4 schedule (drop-in for kernels/generate_meta.py:30-48 / generate_meta_csc.py:14-93
+ * and the .warp4 files read by load_warp4_metadata, cuda_kernel_bindings.cpp:287-317).
+ * maxk_warp4_count: synchronous; number of entries W = sum over rows of ceil(deg/warp_max_nz).
+ * maxk_warp4_build: fills warp4[W*4] on the stream; needs
+ *   maxk_warp4_build_workspace_size(num_rows) bytes of workspace.
+ * maxk_warp4_to_row_ptr: recovers the CSR row_ptr[num_rows+1] a warp4 array
+ *   describes (rows absent from it are empty); lets the reference's
+ *   spmm_maxk_forward(warp4, ...) signature drive the CSR kernels.
+ * ------------------------------------------------------------------------- */
+int maxk_warp4_count(const int32_t *row_ptr, int64_t num_rows, int32_t warp_max_nz,
+                     int64_t *num_entries, void *stream);
+size_t maxk_warp4_build_workspace_size(int64_t num_rows);
+int maxk_warp4_build(const int32_t *row_ptr, int64_t num_rows, int32_t warp_max_nz,
+                     int32_t *warp4, int64_t num_entries, void *workspace,
+                     size_t workspace_bytes, void *stream);
+int maxk_warp4_to_row_ptr(const int32_t *warp4, int64_t num_entries, int64_t num_rows,
+                          int32_t *row_ptr, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Dense SpMM baseline Y = A . X on rocSPARSE (the speed-up denominator; the
+ * MI355X equivalent of spmm_cusparse, kernels/spmm_cusparse.cu:6-62, and of
+ * the cusparse_spmm binding, cuda_kernel_bindings.cpp:253-284).
+ * A plan owns the rocSPARSE handle, descriptors and buffer (synchronous to
+ * create); maxk_dense_spmm_run only launches (alpha=1, beta=0).
+ * ------------------------------------------------------------------------- */
+typedef struct maxk_dense_spmm_plan maxk_dense_spmm_plan;
+int maxk_dense_spmm_plan_create(maxk_dense_spmm_plan **plan, const int32_t *row_ptr,
+                                const int32_t *col_idx, const float *edge_val, const float *x,
+                                float *y, int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                int32_t dim, int32_t alg, void *stream);
+int maxk_dense_spmm_run(maxk_dense_spmm_plan *plan, void *stream);
+int maxk_dense_spmm_plan_destroy(maxk_dense_spmm_plan *plan);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MAXK_HIP_H_ */

@@ -1,0 +1,222 @@
+/*
+ * maxk_oracle.c -- CPU restatement of the MaxK-GNN aggregation hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * product path in spgemm-prunning_amd/csrc.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it, and only as the checker / the
+ * timed CPU baseline -- never as the thing measured or shipped.
+ *
+ * Pinning: the restatement is checked against golden vectors produced by the
+ * reference's own Python code (maxk_spgemm_function.py CPU fallback + autograd,
+ * generate_meta_csc.generate_warp4_metadata) -- see tests/golden/make_golden.py
+ * and tests/test_oracle.py.
+ *
+ * Arithmetic: every sum is accumulated in double in the reference kernels'
+ * traversal order (CSR row order, edge order inside a row, lane order inside an
+ * edge) and rounded to fp32 once at the end.
+ *
+ * Reference semantics restated here (paths relative to the reference root):
+ *   forward  SpGEMM  kernels/spmm_maxk.cu:66-79,85-96,101-105
+ *   backward SSpMM   kernels/spmm_maxk_backward.cu:52-57,69-84,92-103
+ *   warp4 schedule   kernels/generate_meta.py:30-48, generate_meta_csc.py:14-93
+ *   CBSR encode      maxk_spgemm_function.py:51-63 (torch.topk, largest, sorted)
+ *   grad scatter     maxk_spgemm_function.py:152,175
+ *   normalisation    maxk_spgemm_function.py:85-91 (fwd /in_deg), :154-159 (bwd /out_deg)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+void oracle_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
+/*
+ * Forward row-wise-product SpGEMM (kernels/spmm_maxk.cu:17-106).
+ *   out[r, sel[c,l]] += val[e] * data[c,l]   for e in row r, c = col_idx[e], l < k
+ * then out[r,:] /= row_div[r] when row_div != NULL (maxk_spgemm_function.py:85-86).
+ * Rows [r_begin, r_end) only (bounded CPU-baseline samples); pass 0,V for all.
+ * Output rows outside the range are left untouched.
+ */
+void oracle_spgemm_fwd(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                       const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div,
+                       float *out, int64_t V, int32_t D, int32_t k,
+                       int64_t r_begin, int64_t r_end)
+{
+    (void)V;
+#pragma omp parallel
+    {
+        double *acc = (double *)malloc(sizeof(double) * (size_t)D);
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t r = r_begin; r < r_end; ++r) {
+            for (int32_t j = 0; j < D; ++j) acc[j] = 0.0;
+            for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+                const int64_t c = col_idx[e];
+                const double w = (double)val[e];
+                const float *dv = cbsr_val + c * k;
+                const uint8_t *sv = cbsr_idx + c * k;
+                for (int32_t l = 0; l < k; ++l) acc[sv[l]] += w * (double)dv[l];
+            }
+            const double div = row_div ? (double)row_div[r] : 1.0;
+            float *o = out + r * (int64_t)D;
+            for (int32_t j = 0; j < D; ++j) o[j] = (float)(acc[j] / div);
+        }
+        free(acc);
+    }
+}
+
+/*
+ * Backward outer-product SSpMM (kernels/spmm_maxk_backward.cu:15-115), push
+ * formulation exactly as the reference traverses it: stage G[r] (/row_div[r],
+ * maxk_spgemm_function.py:154-155), then for each edge r->c and lane l
+ *   gs[c,l] += val[e] * G[r, sel[c,l]]
+ * Single-threaded: the push scatters into arbitrary rows, and the sum order is
+ * the reference's CSR order.
+ */
+void oracle_sspmm_bwd(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                      const float *grad, const float *row_div, const uint8_t *cbsr_idx,
+                      float *grad_cbsr, int64_t V, int32_t D, int32_t k)
+{
+    double *acc = (double *)calloc((size_t)V * (size_t)k, sizeof(double));
+    double *g = (double *)malloc(sizeof(double) * (size_t)D);
+    for (int64_t r = 0; r < V; ++r) {
+        const float *gr = grad + r * (int64_t)D;
+        for (int32_t j = 0; j < D; ++j)
+            g[j] = row_div ? (double)gr[j] / (double)row_div[r] : (double)gr[j];
+        for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+            const int64_t c = col_idx[e];
+            const double w = (double)val[e];
+            const uint8_t *sv = cbsr_idx + c * k;
+            double *a = acc + c * k;
+            for (int32_t l = 0; l < k; ++l) a[l] += w * g[sv[l]];
+        }
+    }
+    for (int64_t i = 0; i < V * (int64_t)k; ++i) grad_cbsr[i] = (float)acc[i];
+    free(g);
+    free(acc);
+}
+
+/*
+ * Same backward, pull formulation over a caller-built transpose (CSC of A:
+ * t_ptr over destination columns c, t_src = source rows r, t_val = edge
+ * weight), OpenMP-parallel over c.  Used for the timed CPU baseline (a push
+ * cannot be parallelised without atomics) and checked against
+ * oracle_sspmm_bwd in tests.  Columns [c_begin, c_end) only.
+ */
+void oracle_sspmm_bwd_pull(const int32_t *t_ptr, const int32_t *t_src, const float *t_val,
+                           const float *grad, const float *row_div, const uint8_t *cbsr_idx,
+                           float *grad_cbsr, int64_t V, int32_t D, int32_t k,
+                           int64_t c_begin, int64_t c_end)
+{
+    (void)V;
+#pragma omp parallel
+    {
+        double *acc = (double *)malloc(sizeof(double) * (size_t)k);
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t c = c_begin; c < c_end; ++c) {
+            for (int32_t l = 0; l < k; ++l) acc[l] = 0.0;
+            const uint8_t *sv = cbsr_idx + c * k;
+            for (int64_t t = t_ptr[c]; t < t_ptr[c + 1]; ++t) {
+                const int64_t r = t_src[t];
+                const float *gr = grad + r * (int64_t)D;
+                const double w = row_div ? (double)t_val[t] / (double)row_div[r] : (double)t_val[t];
+                for (int32_t l = 0; l < k; ++l) acc[l] += w * (double)gr[sv[l]];
+            }
+            for (int32_t l = 0; l < k; ++l) grad_cbsr[c * k + l] = (float)acc[l];
+        }
+        free(acc);
+    }
+}
+
+/* Order-preserving key of an fp32 value; every NaN maps above +inf, which is
+ * how torch.topk ranks NaN (largest). */
+static inline uint32_t topk_key(float x)
+{
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0xffffffffu;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+/*
+ * CBSR encode = torch.topk(x, k, dim=1, largest=True, sorted=True) then
+ * indices.to(uint8) (maxk_spgemm_function.py:51-57).  Output order: key
+ * descending; equal keys by ascending column (torch leaves tie order
+ * unspecified; fixtures are tie-free).  Selection sort of k out of D per row.
+ */
+void oracle_topk(const float *x, float *val, uint8_t *idx, int64_t V, int32_t D, int32_t k)
+{
+#pragma omp parallel
+    {
+        uint32_t *key = (uint32_t *)malloc(sizeof(uint32_t) * (size_t)D);
+        uint8_t *taken = (uint8_t *)malloc((size_t)D);
+#pragma omp for schedule(static)
+        for (int64_t r = 0; r < V; ++r) {
+            const float *xr = x + r * (int64_t)D;
+            for (int32_t j = 0; j < D; ++j) { key[j] = topk_key(xr[j]); taken[j] = 0; }
+            for (int32_t p = 0; p < k; ++p) {
+                int32_t best = -1;
+                for (int32_t j = 0; j < D; ++j)
+                    if (!taken[j] && (best < 0 || key[j] > key[best])) best = j;
+                taken[best] = 1;
+                val[r * k + p] = xr[best];
+                idx[r * k + p] = (uint8_t)best;
+            }
+        }
+        free(taken);
+        free(key);
+    }
+}
+
+/*
+ * warp4 schedule (kernels/generate_meta.py:30-48): every non-empty CSR row is
+ * cut into chunks of <= warp_max_nz edges, each emitted as (row, loc, len, 0).
+ * Returns the number of entries W; writes min(W, cap) entries to out[4*W].
+ */
+int64_t oracle_warp4(const int32_t *row_ptr, int64_t V, int32_t warp_max_nz,
+                     int32_t *out, int64_t cap)
+{
+    int64_t w = 0;
+    for (int64_t r = 0; r < V; ++r) {
+        int64_t loc = row_ptr[r];
+        const int64_t end = row_ptr[r + 1];
+        while (loc < end) {
+            const int64_t len = (end - loc) < warp_max_nz ? (end - loc) : warp_max_nz;
+            if (w < cap) {
+                out[4 * w + 0] = (int32_t)r;
+                out[4 * w + 1] = (int32_t)loc;
+                out[4 * w + 2] = (int32_t)len;
+                out[4 * w + 3] = 0;
+            }
+            ++w;
+            loc += len;
+        }
+    }
+    return w;
+}
+
+/* grad_input = zeros(V,D).scatter_(1, sel, grad_cbsr) (maxk_spgemm_function.py:152,175). */
+void oracle_scatter_dense(const float *grad_cbsr, const uint8_t *cbsr_idx, float *dense,
+                          int64_t V, int32_t D, int32_t k)
+{
+    memset(dense, 0, sizeof(float) * (size_t)V * (size_t)D);
+    for (int64_t r = 0; r < V; ++r)
+        for (int32_t l = 0; l < k; ++l)
+            dense[r * D + cbsr_idx[r * k + l]] = grad_cbsr[r * k + l];
+}

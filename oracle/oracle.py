@@ -1,0 +1,165 @@
+"""CPU oracle for the MaxK-GNN aggregation hot path -- TEST INFRASTRUCTURE ONLY.
+
+numpy front-end over ``oracle/maxk_oracle.c`` (built by ``oracle/Makefile`` into
+``oracle/_build/liboracle.so``).  Only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import this module, and only as the
+checker or the timed CPU baseline.  The product path
+(``spgemm-prunning_amd/``) never imports it.
+
+Every function cites the reference code it restates; the C file holds the
+arithmetic.  Pinned against the reference's own Python code by
+``tests/golden/*.npz`` (generator: ``tests/golden/make_golden.py``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+
+
+def build() -> str:
+    """Compile the oracle (gcc) if needed; returns the .so path."""
+    src = os.path.join(_HERE, "maxk_oracle.c")
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(build())
+        L.oracle_spgemm_fwd.argtypes = [_i32p, _i32p, _f32p, _f32p, _u8p, ctypes.c_void_p,
+                                        _f32p, _i64, _i32, _i32, _i64, _i64]
+        L.oracle_sspmm_bwd.argtypes = [_i32p, _i32p, _f32p, _f32p, ctypes.c_void_p, _u8p,
+                                       _f32p, _i64, _i32, _i32]
+        L.oracle_sspmm_bwd_pull.argtypes = [_i32p, _i32p, _f32p, _f32p, ctypes.c_void_p, _u8p,
+                                            _f32p, _i64, _i32, _i32, _i64, _i64]
+        L.oracle_topk.argtypes = [_f32p, _f32p, _u8p, _i64, _i32, _i32]
+        L.oracle_warp4.argtypes = [_i32p, _i64, _i32, ctypes.c_void_p, _i64]
+        L.oracle_warp4.restype = _i64
+        L.oracle_scatter_dense.argtypes = [_f32p, _u8p, _f32p, _i64, _i32, _i32]
+        L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_set_num_threads.argtypes = [ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def _opt_f32(a):
+    if a is None:
+        return None, None
+    a = _c(a, np.float32)
+    return a, a.ctypes.data_as(ctypes.c_void_p)
+
+
+def num_threads() -> int:
+    return lib().oracle_num_threads()
+
+
+def set_num_threads(n: int) -> None:
+    lib().oracle_set_num_threads(int(n))
+
+
+def spgemm_fwd(row_ptr, col_idx, val, cbsr_val, cbsr_idx, D, row_div=None, rows=None):
+    """Forward SpGEMM, kernels/spmm_maxk.cu:66-105 (+ /in_deg, maxk_spgemm_function.py:85-86).
+
+    Returns fp32 [V, D].  ``rows=(r0, r1)`` computes only that row range (the
+    other rows are returned as zeros) -- the bounded CPU-baseline sample.
+    """
+    row_ptr, col_idx, val = _c(row_ptr, np.int32), _c(col_idx, np.int32), _c(val, np.float32)
+    cbsr_val, cbsr_idx = _c(cbsr_val, np.float32), _c(cbsr_idx, np.uint8)
+    V = row_ptr.shape[0] - 1
+    k = cbsr_val.shape[1] if cbsr_val.ndim == 2 else int(cbsr_val.size // max(V, 1))
+    r0, r1 = (0, V) if rows is None else rows
+    out = np.zeros((V, D), dtype=np.float32)
+    keep, div = _opt_f32(row_div)
+    lib().oracle_spgemm_fwd(row_ptr, col_idx, val, cbsr_val, cbsr_idx, div, out, V, D, k, r0, r1)
+    del keep
+    return out
+
+
+def sspmm_bwd(row_ptr, col_idx, val, grad, cbsr_idx, row_div=None):
+    """Backward SSpMM in the reference's push order, kernels/spmm_maxk_backward.cu:52-103
+    (G / out_deg first, maxk_spgemm_function.py:154-155).  Returns fp32 [V, k]."""
+    row_ptr, col_idx, val = _c(row_ptr, np.int32), _c(col_idx, np.int32), _c(val, np.float32)
+    grad, cbsr_idx = _c(grad, np.float32), _c(cbsr_idx, np.uint8)
+    V, D = grad.shape
+    k = cbsr_idx.shape[1]
+    out = np.zeros((V, k), dtype=np.float32)
+    keep, div = _opt_f32(row_div)
+    lib().oracle_sspmm_bwd(row_ptr, col_idx, val, grad, div, cbsr_idx, out, V, D, k)
+    del keep
+    return out
+
+
+def transpose_csr(row_ptr, col_idx, val, V=None):
+    """CSR of A -> CSR of A^T (t_ptr over columns, t_src = rows), stable in row order."""
+    row_ptr = np.asarray(row_ptr, dtype=np.int64)
+    col_idx = np.asarray(col_idx, dtype=np.int64)
+    V = row_ptr.shape[0] - 1 if V is None else V
+    rows = np.repeat(np.arange(V, dtype=np.int64), np.diff(row_ptr))
+    order = np.argsort(col_idx, kind="stable")
+    t_ptr = np.zeros(V + 1, dtype=np.int64)
+    np.cumsum(np.bincount(col_idx, minlength=V), out=t_ptr[1:])
+    return (t_ptr.astype(np.int32), rows[order].astype(np.int32),
+            np.asarray(val, dtype=np.float32)[order])
+
+
+def sspmm_bwd_pull(t_ptr, t_src, t_val, grad, cbsr_idx, row_div=None, cols=None):
+    """Backward via the transpose (pull), OpenMP; same sums as :func:`sspmm_bwd`.
+    ``cols=(c0, c1)`` computes only those output rows (bounded baseline sample)."""
+    t_ptr, t_src, t_val = _c(t_ptr, np.int32), _c(t_src, np.int32), _c(t_val, np.float32)
+    grad, cbsr_idx = _c(grad, np.float32), _c(cbsr_idx, np.uint8)
+    V, D = grad.shape
+    k = cbsr_idx.shape[1]
+    c0, c1 = (0, V) if cols is None else cols
+    out = np.zeros((V, k), dtype=np.float32)
+    keep, div = _opt_f32(row_div)
+    lib().oracle_sspmm_bwd_pull(t_ptr, t_src, t_val, grad, div, cbsr_idx, out, V, D, k, c0, c1)
+    del keep
+    return out
+
+
+def topk(x, k):
+    """CBSR encode = torch.topk(x, k, dim=1) + .to(uint8), maxk_spgemm_function.py:51-57."""
+    x = _c(x, np.float32)
+    V, D = x.shape
+    val = np.zeros((V, k), dtype=np.float32)
+    idx = np.zeros((V, k), dtype=np.uint8)
+    lib().oracle_topk(x, val, idx, V, D, k)
+    return val, idx
+
+
+def warp4(row_ptr, warp_max_nz=64):
+    """warp4 schedule, kernels/generate_meta.py:30-48.  Returns int32 [W*4] (flat, as on disk)."""
+    row_ptr = _c(row_ptr, np.int32)
+    V = row_ptr.shape[0] - 1
+    W = lib().oracle_warp4(row_ptr, V, warp_max_nz, None, 0)
+    out = np.zeros(4 * W, dtype=np.int32)
+    lib().oracle_warp4(row_ptr, V, warp_max_nz, out.ctypes.data_as(ctypes.c_void_p), W)
+    return out
+
+
+def scatter_dense(grad_cbsr, cbsr_idx, D):
+    """zeros(V,D).scatter_(1, sel, grad_cbsr), maxk_spgemm_function.py:152,175."""
+    grad_cbsr, cbsr_idx = _c(grad_cbsr, np.float32), _c(cbsr_idx, np.uint8)
+    V, k = grad_cbsr.shape
+    out = np.zeros((V, D), dtype=np.float32)
+    lib().oracle_scatter_dense(grad_cbsr, cbsr_idx, out, V, D, k)
+    return out

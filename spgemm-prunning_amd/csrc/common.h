@@ -1,0 +1,103 @@
+// Shared host/device helpers for libmaxk_hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "maxk_hip.h"
+
+namespace maxk {
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows are 256 floats
+
+// ---- error reporting (host) ----
+void set_error(const char *fmt, ...);
+void clear_error();
+
+#define MAXK_REQUIRE(cond, ...)                  \
+    do {                                         \
+        if (!(cond)) {                           \
+            ::maxk::set_error(__VA_ARGS__);      \
+            return MAXK_ERR_INVALID;             \
+        }                                        \
+    } while (0)
+
+#define MAXK_HIP(call)                                                              \
+    do {                                                                            \
+        hipError_t e_ = (call);                                                     \
+        if (e_ != hipSuccess) {                                                     \
+            ::maxk::set_error("%s failed: %s", #call, hipGetErrorString(e_));       \
+            return MAXK_ERR_HIP;                                                    \
+        }                                                                           \
+    } while (0)
+
+// After a launch: report a launch error (never synchronises).
+#define MAXK_LAUNCHED(name)                                                         \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) {                                                     \
+            ::maxk::set_error("%s launch failed: %s", name, hipGetErrorString(e_)); \
+            return MAXK_ERR_HIP;                                                    \
+        }                                                                           \
+    } while (0)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Lanes per edge group: next power of two >= k, capped at a wave.
+inline int lanes_per_edge(int k) {
+    int g = 1;
+    while (g < k && g < kWave) g <<= 1;
+    return g;
+}
+
+// ---- device helpers ----
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Orders this wave's LDS traffic at a phase change (all lanes of ONE wave):
+// LDS executes a wave's instructions in order; this only stops the compiler
+// from moving LDS accesses across the boundary.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Token-stream work partition shared by the SpGEMM/SSpMM kernels: row r's token
+// sits at r + row_ptr[r], edge e of row q at e + q + 1; a work item owns a
+// contiguous token range.  Returns the first r in [0, n] whose token is >= d
+// (row_ptr[n] + n >= d required).  64-ary search by the whole wave; the result
+// is wave-uniform.
+__device__ __forceinline__ int wave_first_row_token(const int32_t *__restrict__ row_ptr, int n,
+                                                    int64_t d) {
+    const int lane = lane_id();
+    int lo = 0, hi = n;  // answer in [lo, hi]
+    while (hi - lo > 63) {
+        const int step = (hi - lo + 62) / 63;  // lo + 63*step >= hi
+        int p = lo + lane * step;
+        p = p > hi ? hi : p;
+        const uint64_t m = __ballot((int64_t)row_ptr[p] + p >= d);  // lane 63 probes hi: true
+        const int f = __builtin_ctzll(m);
+        if (f == 0) {
+            hi = lo;
+        } else {
+            const int pf = lo + f * step;
+            lo = lo + (f - 1) * step + 1;
+            hi = pf > hi ? hi : pf;
+        }
+    }
+    const int p = lo + lane;
+    const int pc = p > hi ? hi : p;
+    const uint64_t m = __ballot(p <= hi && (int64_t)row_ptr[pc] + pc >= d) | (1ull << 63);
+    const int r = lo + __builtin_ctzll(m);
+    return r > hi ? hi : r;
+}
+
+}  // namespace maxk

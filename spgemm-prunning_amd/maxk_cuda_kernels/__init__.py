@@ -1,0 +1,446 @@
+"""maxk_cuda_kernels -- MI355X-native drop-in for the reference extension of the same name.
+
+Same function names, argument names, defaults and return shapes as the
+reference's pybind11 module (cuda_kernel_bindings.cpp:429-490, plus the v2
+additions load_warp4_metadata_csc / validate_spmm_maxk_backward,
+binding_v2.py:320-351,464-486).  Every compute call goes to hand-written HIP
+kernels for gfx950 in libmaxk_hip.so through its C ABI (include/maxk_hip.h);
+there is no CPU or PyTorch fallback.
+
+Differences from the reference, all deliberate (DESIGN.md "Boundary"):
+  * launches go on torch's *current* HIP stream, not the legacy default stream;
+  * `dim_origin` (the dense width D) is a keyword argument defaulting to the
+    reference's hard-coded 256 (cuda_kernel_bindings.cpp:70) instead of a constant;
+  * the kernels consume the CSR row_ptr; `spmm_maxk_forward/backward` accept the
+    reference's warp4 metadata and derive row_ptr from it on the GPU (or take
+    `indptr=` directly);
+  * results are exact for every k in [1, D] (the reference drops rows / reads
+    stale shared memory for k < 32);
+  * cuda_topk_maxk_float is an exact top-k (the reference quantises to uint8).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _capi
+
+_capi.load()  # ImportError here <=> extension missing (callers test this, like the reference)
+
+__all__ = [
+    "spmm_maxk_forward", "spmm_maxk_backward", "cuda_topk_maxk", "cuda_topk_maxk_float",
+    "prepare_cbsr_format_maxk", "cusparse_spmm", "load_warp4_metadata",
+    "load_warp4_metadata_csc", "generate_sparse_selector", "benchmark_spmm_maxk",
+    "validate_spmm_maxk", "validate_spmm_maxk_backward", "CudaTimer",
+    # MI355X additions
+    "topk_cbsr", "cbsr_scatter_dense", "build_warp4_metadata", "warp4_to_indptr",
+    "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
+]
+
+FULL_DIM = 256  # the reference binding's fixed output width (cuda_kernel_bindings.cpp:70)
+
+
+def _lib():
+    return _capi.load()
+
+
+def version() -> int:
+    return _lib().maxk_version()
+
+
+def device_count() -> int:
+    return _lib().maxk_device_count()
+
+
+def _validate_default() -> bool:
+    return os.environ.get("MAXK_VALIDATE", "0") not in ("", "0")
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() > 0 else None
+
+
+def _need(t, name, dtype=None):
+    if not isinstance(t, torch.Tensor):
+        raise RuntimeError(f"{name} must be a tensor")
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be CUDA tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise RuntimeError(f"{name} must be {str(dtype).replace('torch.', '')}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _validate_graph(row_ptr, col_idx, num_cols, num_e):
+    if row_ptr.numel() == 0:
+        raise RuntimeError("row_ptr must have num_rows+1 entries")
+    if int(row_ptr[0]) != 0 or int(row_ptr[-1]) != num_e:
+        raise RuntimeError(f"row_ptr must start at 0 and end at num_e={num_e}")
+    if row_ptr.numel() > 1 and bool((row_ptr[1:] < row_ptr[:-1]).any()):
+        raise RuntimeError("row_ptr must be non-decreasing")
+    if num_e and (int(col_idx.min()) < 0 or int(col_idx.max()) >= num_cols):
+        raise RuntimeError(f"col_idx out of range [0, {num_cols})")
+
+
+def _validate_selector(sel, D):
+    if sel.numel() and int(sel.max()) >= D:
+        raise RuntimeError(f"sparse_selector entries must be < dim_origin={D}")
+
+
+# --------------------------------------------------------------------------- schedule
+def warp4_to_indptr(warp4_metadata: torch.Tensor, num_v: int,
+                    num_warps: Optional[int] = None) -> torch.Tensor:
+    """CSR row_ptr [num_v+1] described by a warp4 array (first `num_warps` entries)."""
+    _need(warp4_metadata, "warp4_metadata", torch.int32)
+    W = warp4_metadata.numel() // 4 if num_warps is None else min(int(num_warps),
+                                                                   warp4_metadata.numel() // 4)
+    row_ptr = torch.empty(num_v + 1, dtype=torch.int32, device=warp4_metadata.device)
+    with torch.cuda.device(warp4_metadata.device):
+        _capi.check(_lib().maxk_warp4_to_row_ptr(_ptr(warp4_metadata), W, num_v, _ptr(row_ptr),
+                                                 _stream(warp4_metadata.device)),
+                    "maxk_warp4_to_row_ptr")
+    return row_ptr
+
+
+def build_warp4_metadata(indptr: torch.Tensor, warp_max_nz: int = 64) -> torch.Tensor:
+    """warp4 schedule built on the GPU (kernels/generate_meta.py:30-48 semantics).
+    Returns flat int32 [4W] on the device of `indptr` -- the layout of a .warp4 file."""
+    _need(indptr, "indptr", torch.int32)
+    dev = indptr.device
+    V = indptr.numel() - 1
+    with torch.cuda.device(dev):
+        s = _stream(dev)
+        n = ctypes.c_int64(0)
+        _capi.check(_lib().maxk_warp4_count(_ptr(indptr), V, warp_max_nz, ctypes.byref(n), s),
+                    "maxk_warp4_count")
+        out = torch.empty(4 * n.value, dtype=torch.int32, device=dev)
+        ws = torch.empty(max(1, _lib().maxk_warp4_build_workspace_size(V)), dtype=torch.uint8,
+                         device=dev)
+        _capi.check(_lib().maxk_warp4_build(_ptr(indptr), V, warp_max_nz, _ptr(out), n.value,
+                                            _ptr(ws), ws.numel(), s), "maxk_warp4_build")
+    return out
+
+
+def _read_warp4_file(path: str, device="cuda") -> torch.Tensor:
+    if not os.path.exists(path):
+        raise RuntimeError(f"Cannot open warp4 file: {path}")
+    import numpy as np
+    data = np.fromfile(path, dtype=np.int32)
+    return torch.from_numpy(data).to(device)
+
+
+def load_warp4_metadata(graph_name: str, num_warps: int = 12, warp_max_nz: int = 64) -> torch.Tensor:
+    """Read kernels/w{num_warps}_nz{warp_max_nz}_warp_4/<graph>.warp4 (CWD-relative) into
+    an int32 CUDA tensor -- cuda_kernel_bindings.cpp:287-317."""
+    path = f"kernels/w{num_warps}_nz{warp_max_nz}_warp_4/{graph_name}.warp4"
+    return _read_warp4_file(path)
+
+
+def load_warp4_metadata_csc(graph_name: str, num_warps: int = 12,
+                            warp_max_nz: int = 64) -> torch.Tensor:
+    """CSC twin, binding_v2.py:320-351 (kernels/w12_nz64_warp_4_csc/<graph>.warp4_csc)."""
+    path = f"kernels/w{num_warps}_nz{warp_max_nz}_warp_4_csc/{graph_name}.warp4_csc"
+    return _read_warp4_file(path)
+
+
+# --------------------------------------------------------------------------- hot path
+def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                   cbsr_val: torch.Tensor, cbsr_idx: torch.Tensor, dim_origin: int,
+                   row_div: Optional[torch.Tensor] = None, chunk: int = 0,
+                   out: Optional[torch.Tensor] = None, validate: Optional[bool] = None
+                   ) -> torch.Tensor:
+    """out[num_rows, D] = diag(1/row_div) . A . scatter(cbsr)  (CSR A: indptr/indices/values)."""
+    for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
+                     (values, "values", torch.float32), (cbsr_val, "input_data", torch.float32),
+                     (cbsr_idx, "sparse_selector", torch.uint8)):
+        _need(t, n, dt)
+    num_rows = indptr.numel() - 1
+    num_cols, k = (cbsr_val.shape[0], cbsr_val.shape[1]) if cbsr_val.dim() == 2 else (0, 0)
+    if cbsr_idx.shape != cbsr_val.shape:
+        raise RuntimeError("input_data and sparse_selector must have the same [V, k] shape")
+    if values.numel() != indices.numel():
+        raise RuntimeError("values and indices must have the same length")
+    D = int(dim_origin)
+    if row_div is not None:
+        _need(row_div, "row_div", torch.float32)
+        if row_div.numel() != num_rows:
+            raise RuntimeError("row_div must have num_rows entries")
+    if validate if validate is not None else _validate_default():
+        _validate_graph(indptr, indices, num_cols, indices.numel())
+        _validate_selector(cbsr_idx, D)
+    dev = cbsr_val.device
+    if out is None:
+        out = torch.empty(num_rows, D, dtype=torch.float32, device=dev)
+    else:
+        _need(out, "out", torch.float32)
+        if tuple(out.shape) != (num_rows, D):
+            raise RuntimeError("out must be [num_rows, dim_origin]")
+    L = _lib()
+    E = indices.numel()
+    ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, E, D, k, chunk)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(L.maxk_spgemm_forward(
+            _ptr(indptr), _ptr(indices), _ptr(values), _ptr(cbsr_val), _ptr(cbsr_idx),
+            _ptr(row_div), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws), ws.numel(),
+            _stream(dev)), "maxk_spgemm_forward")
+    return out
+
+
+def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                   grad_output: torch.Tensor, cbsr_idx: torch.Tensor,
+                   row_div: Optional[torch.Tensor] = None, chunk: int = 0,
+                   out: Optional[torch.Tensor] = None, validate: Optional[bool] = None
+                   ) -> torch.Tensor:
+    """grad_cbsr[num_cols, k] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]]."""
+    for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
+                     (values, "values", torch.float32), (grad_output, "grad_output", torch.float32),
+                     (cbsr_idx, "sparse_selector", torch.uint8)):
+        _need(t, n, dt)
+    num_rows = indptr.numel() - 1
+    if grad_output.dim() != 2 or grad_output.shape[0] != num_rows:
+        raise RuntimeError("grad_output must be [num_rows, dim_origin]")
+    D = grad_output.shape[1]
+    num_cols, k = cbsr_idx.shape
+    if row_div is not None:
+        _need(row_div, "row_div", torch.float32)
+        if row_div.numel() != num_rows:
+            raise RuntimeError("row_div must have num_rows entries")
+    if validate if validate is not None else _validate_default():
+        _validate_graph(indptr, indices, num_cols, indices.numel())
+        _validate_selector(cbsr_idx, D)
+    dev = grad_output.device
+    if out is None:
+        out = torch.empty(num_cols, k, dtype=torch.float32, device=dev)
+    else:
+        _need(out, "out", torch.float32)
+        if tuple(out.shape) != (num_cols, k):
+            raise RuntimeError("out must be [num_cols, k]")
+    L = _lib()
+    E = indices.numel()
+    ws_bytes = L.maxk_sspmm_backward_workspace_size(num_rows, num_cols, E, D, k, chunk)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(L.maxk_sspmm_backward(
+            _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
+            _ptr(cbsr_idx), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws), ws.numel(),
+            _stream(dev)), "maxk_sspmm_backward")
+    return out
+
+
+def spmm_maxk_forward(warp4_metadata: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                      input_data: torch.Tensor, sparse_selector: torch.Tensor, num_warps: int,
+                      dim_sparse: int, *, dim_origin: int = FULL_DIM,
+                      indptr: Optional[torch.Tensor] = None,
+                      row_div: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """MaxK forward SpGEMM (cuda_kernel_bindings.cpp:42-104): returns f32 [V, dim_origin]."""
+    _need(input_data, "input_data", torch.float32)
+    if input_data.dim() != 2 or input_data.shape[1] != dim_sparse:
+        raise RuntimeError("input_data must be [V, dim_sparse]")
+    if indptr is None:
+        indptr = warp4_to_indptr(warp4_metadata, input_data.shape[0], num_warps)
+    return spgemm_forward(indptr, indices, values, input_data, sparse_selector, dim_origin,
+                          row_div=row_div)
+
+
+def spmm_maxk_backward(warp4_metadata: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                       grad_output: torch.Tensor, sparse_selector: torch.Tensor, num_warps: int,
+                       dim_sparse: int, *, indptr: Optional[torch.Tensor] = None,
+                       row_div: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """MaxK backward SSpMM (cuda_kernel_bindings.cpp:106-161): returns f32 [V, dim_sparse]."""
+    _need(grad_output, "grad_output", torch.float32)
+    _need(sparse_selector, "sparse_selector", torch.uint8)
+    if sparse_selector.dim() != 2 or sparse_selector.shape[1] != dim_sparse:
+        raise RuntimeError("sparse_selector must be [V, dim_sparse]")
+    if indptr is None:
+        indptr = warp4_to_indptr(warp4_metadata, grad_output.shape[0], num_warps)
+    return sspmm_backward(indptr, indices, values, grad_output, sparse_selector, row_div=row_div)
+
+
+# --------------------------------------------------------------------------- CBSR encode
+def topk_cbsr(x: torch.Tensor, k: int, with_int32: bool = False):
+    """(values, uint8 indices[, int32 indices]) = torch.topk(x, k, dim=1) on the GPU kernel."""
+    if x.dim() != 2:
+        raise RuntimeError("Input must be 2D tensor")
+    if not x.is_cuda:
+        raise RuntimeError("Input must be on CUDA")
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    V, D = x.shape
+    if not (0 < k <= D):
+        raise RuntimeError("Invalid k value")
+    dev = x.device
+    val = torch.empty(V, k, dtype=x.dtype, device=dev)
+    idx = torch.empty(V, k, dtype=torch.uint8, device=dev)
+    idx32 = torch.empty(V, k, dtype=torch.int32, device=dev) if with_int32 else None
+    L = _lib()
+    if x.dtype == torch.float32:
+        fn, name = L.maxk_topk_cbsr, "maxk_topk_cbsr"
+    elif x.dtype == torch.uint8:
+        fn, name = L.maxk_topk_cbsr_u8, "maxk_topk_cbsr_u8"
+    else:
+        raise RuntimeError("Input must be float32 or uint8")
+    with torch.cuda.device(dev):
+        _capi.check(fn(_ptr(x), x.stride(0), _ptr(val), _ptr(idx), _ptr(idx32), V, D, k,
+                       _stream(dev)), name)
+    return (val, idx, idx32) if with_int32 else (val, idx)
+
+
+def cuda_topk_maxk(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """uint8 top-k (cuda_kernel_bindings.cpp:164-201): (values u8 [N,k], indices u8 [N,k])."""
+    if input.dtype != torch.uint8:
+        raise RuntimeError("Input must be uint8 tensor")
+    return topk_cbsr(input, k)
+
+
+def cuda_topk_maxk_float(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(values, int32 indices) (cuda_kernel_bindings.cpp:203-238), exact (no uint8 quantisation)."""
+    val, _, idx32 = topk_cbsr(input, k, with_int32=True)
+    return val, idx32
+
+
+def prepare_cbsr_format_maxk(features: torch.Tensor, maxk: int):
+    """(sparse_data, sparse_indices) (cuda_kernel_bindings.cpp:240-251)."""
+    return cuda_topk_maxk_float(features, maxk)
+
+
+def cbsr_scatter_dense(cbsr_val: torch.Tensor, cbsr_idx: torch.Tensor, dim_origin: int,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """zeros(V, D).scatter_(1, idx, val) in one HIP pass (maxk_spgemm_function.py:152,175)."""
+    _need(cbsr_val, "cbsr_val", torch.float32)
+    _need(cbsr_idx, "cbsr_idx", torch.uint8)
+    V, k = cbsr_val.shape
+    dev = cbsr_val.device
+    if out is None:
+        out = torch.empty(V, dim_origin, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(_lib().maxk_cbsr_scatter_dense(_ptr(cbsr_val), _ptr(cbsr_idx), _ptr(out), V,
+                                                   dim_origin, k, _stream(dev)),
+                    "maxk_cbsr_scatter_dense")
+    return out
+
+
+def generate_sparse_selector(num_v: int, dim_origin: int, dim_sparse: int) -> torch.Tensor:
+    """k distinct random columns per row, seed 123 (cuda_kernel_bindings.cpp:320-340).
+    Same distribution as the reference's per-row randperm; not the same random stream."""
+    gen = torch.Generator(device="cuda").manual_seed(123)
+    keys = torch.rand(num_v, dim_origin, generator=gen, device="cuda")
+    return topk_cbsr(keys, dim_sparse)[1]
+
+
+# --------------------------------------------------------------------------- baseline
+class DenseSpMMPlan:
+    """rocSPARSE Y = A . X (the reference's cuSPARSE denominator, kernels/spmm_cusparse.cu:6-62).
+    Buffers are bound at construction; run() launches on the current stream."""
+
+    def __init__(self, indptr, indices, values, x, y=None, alg: int = 0):
+        for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
+                         (values, "values", torch.float32), (x, "input_features", torch.float32)):
+            _need(t, n, dt)
+        self.num_rows = indptr.numel() - 1
+        self.x = x
+        self.y = y if y is not None else torch.empty(self.num_rows, x.shape[1],
+                                                     dtype=torch.float32, device=x.device)
+        self._keep = (indptr, indices, values)
+        self.device = x.device
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _capi.check(_lib().maxk_dense_spmm_plan_create(
+                ctypes.byref(h), _ptr(indptr), _ptr(indices), _ptr(values), _ptr(x),
+                _ptr(self.y), self.num_rows, x.shape[0], indices.numel(), x.shape[1], alg,
+                _stream(self.device)), "maxk_dense_spmm_plan_create")
+        self._h = h
+
+    def run(self) -> torch.Tensor:
+        with torch.cuda.device(self.device):
+            _capi.check(_lib().maxk_dense_spmm_run(self._h, _stream(self.device)),
+                        "maxk_dense_spmm_run")
+        return self.y
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib().maxk_dense_spmm_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def cusparse_spmm(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                  input_features: torch.Tensor, timing: bool = False) -> torch.Tensor:
+    """Dense SpMM reference (cuda_kernel_bindings.cpp:253-284), here on rocSPARSE."""
+    plan = DenseSpMMPlan(indptr, indices, values, input_features)
+    try:
+        runs = 10 if timing else 1  # the reference's `timing` only repeats the call
+        for _ in range(runs):
+            plan.run()
+        return plan.y
+    finally:
+        plan.close()
+
+
+# --------------------------------------------------------------------------- harness helpers
+class CudaTimer:
+    """Event timer (cuda_kernel_bindings.cpp:343-369) on the current stream; stop() -> ms."""
+
+    def __init__(self):
+        self._a = torch.cuda.Event(enable_timing=True)
+        self._b = torch.cuda.Event(enable_timing=True)
+
+    def start(self):
+        self._a.record()
+
+    def stop(self) -> float:
+        self._b.record()
+        self._b.synchronize()
+        return self._a.elapsed_time(self._b)
+
+
+def benchmark_spmm_maxk(warp4_metadata, indices, values, input_data, sparse_selector,
+                        num_warps: int, dim_sparse: int, num_runs: int = 4) -> List[float]:
+    """num_runs warmup + num_runs timed forward calls (cuda_kernel_bindings.cpp:372-402)."""
+    indptr = warp4_to_indptr(warp4_metadata, input_data.shape[0], num_warps)
+    for _ in range(num_runs):
+        spmm_maxk_forward(warp4_metadata, indices, values, input_data, sparse_selector, num_warps,
+                          dim_sparse, indptr=indptr)
+    torch.cuda.synchronize()
+    times, timer = [], CudaTimer()
+    for _ in range(num_runs):
+        timer.start()
+        spmm_maxk_forward(warp4_metadata, indices, values, input_data, sparse_selector, num_warps,
+                          dim_sparse, indptr=indptr)
+        times.append(timer.stop())
+    return times
+
+
+def validate_spmm_maxk(warp4_metadata, indices, values, input_data, sparse_selector,
+                       reference_output, num_warps: int, dim_sparse: int,
+                       tolerance: float = 0.001) -> bool:
+    """mean |out - reference| < tolerance (cuda_kernel_bindings.cpp:405-427)."""
+    out = spmm_maxk_forward(warp4_metadata, indices, values, input_data, sparse_selector,
+                            num_warps, dim_sparse, dim_origin=reference_output.shape[1])
+    diff = (out - reference_output).abs()
+    print(f"Validation - Max diff: {diff.max().item()}, Avg diff: {diff.mean().item()}")
+    return diff.mean().item() < tolerance
+
+
+def validate_spmm_maxk_backward(warp4_metadata_csc, indices_csc, values_csc, grad_output,
+                                sparse_selector, reference_grad_input, num_warps_csc: int,
+                                dim_sparse: int, tolerance: float = 0.001) -> bool:
+    """mean |grad - reference| < tolerance (binding_v2.py:464-486).  The arrays are the CSR of
+    the forward graph: the kernel forms the A^T product itself."""
+    g = spmm_maxk_backward(warp4_metadata_csc, indices_csc, values_csc, grad_output,
+                           sparse_selector, num_warps_csc, dim_sparse)
+    diff = (g - reference_grad_input).abs()
+    print(f"Backward Validation - Max diff: {diff.max().item()}, Avg diff: {diff.mean().item()}")
+    return diff.mean().item() < tolerance

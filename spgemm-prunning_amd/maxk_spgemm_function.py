@@ -1,0 +1,247 @@
+"""maxk_spgemm_function -- drop-in autograd surface of the MaxK-GNN aggregation.
+
+Mirrors the reference module of the same name (maxk_spgemm_function.py) and its
+v4 successor (spgemmfunction_v4): `MAXK_KERNELS_AVAILABLE`,
+`MaxKSpGEMMFunction`, `maxk_spgemm`, `MaxKSpmmWrapper`.  Both call shapes are
+accepted, told apart by the 4th argument:
+
+  v1  (graph_indices, graph_values, input_features, k_value:int,
+       warp4_metadata=None, num_warps=0, graph_indptr=None, in_degrees=None,
+       out_degrees=None, graph_indices_T=None, graph_values_T=None)
+      -> dense [V, D] = A . topk_scatter(input_features) / in_degrees;
+         grad w.r.t. input_features (maxk_spgemm_function.py:26-184)
+  v4  (graph_indices, graph_values, topk_values, topk_indices:Tensor,
+       warp4_metadata, num_warps, graph_indptr, degrees[, dim_origin])
+      -> dense [V, 256] = A . scatter(topk) / degrees;
+         grad w.r.t. topk_values (spgemmfunction_v4:26-101)
+
+All compute runs in the HIP kernels of maxk_cuda_kernels (libmaxk_hip.so):
+top-k/CBSR encode, forward SpGEMM with the degree division fused into its
+write-back, backward SSpMM with the division fused into its G staging, and the
+CBSR->dense gradient scatter.  When the extension is missing,
+MAXK_KERNELS_AVAILABLE is False and every call raises -- there is no
+torch.sparse / cuSPARSE fallback (a CPU fallback would void parity).
+
+Fixed caller-visible defects of the reference (DESIGN.md "Boundary"):
+  * v1 backward unpacked 7 saved tensors out of 3 (ValueError); here it works;
+  * the backward divides by the same per-row divisor the forward used, so the
+    gradient is the exact adjoint (the reference divides by out_degrees; for
+    the symmetric graphs it targets in == out);
+  * graph_indices_T / graph_values_T are accepted and unused: the kernel forms
+    the A^T product from the CSR itself.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch.autograd import Function
+
+try:
+    import maxk_cuda_kernels
+    MAXK_KERNELS_AVAILABLE = True
+except ImportError as _exc:  # the reference prints and degrades; we refuse to compute
+    maxk_cuda_kernels = None
+    MAXK_KERNELS_AVAILABLE = False
+    _IMPORT_ERROR = str(_exc)
+
+FULL_DIM = 256
+
+
+def _require_kernels():
+    if not MAXK_KERNELS_AVAILABLE:
+        raise RuntimeError("MaxK HIP kernels (maxk_cuda_kernels / libmaxk_hip.so) are not "
+                           f"available: {_IMPORT_ERROR}")
+
+
+def _i32(t):
+    t = t if t.dtype == torch.int32 else t.int()
+    return t.contiguous()
+
+
+def _indptr_for(graph_indptr, warp4_metadata, num_warps, num_v):
+    if graph_indptr is not None:
+        return _i32(graph_indptr)
+    if warp4_metadata is None:
+        raise RuntimeError("MaxK SpGEMM needs graph_indptr or warp4_metadata")
+    return maxk_cuda_kernels.warp4_to_indptr(warp4_metadata, num_v, num_warps or None)
+
+
+def _f32(t):
+    if t is None:
+        return None
+    t = t.float() if t.dtype != torch.float32 else t
+    return t.contiguous()
+
+
+class MaxKSpGEMMFunction(Function):
+    """Autograd function over the HIP forward SpGEMM / backward SSpMM (both call shapes)."""
+
+    @staticmethod
+    def forward(ctx, graph_indices, graph_values, a3, a4, *rest):
+        _require_kernels()
+        graph_indices = _i32(graph_indices)
+        if isinstance(a4, torch.Tensor):
+            out = MaxKSpGEMMFunction._forward_v4(ctx, graph_indices, graph_values, a3, a4, *rest)
+        else:
+            out = MaxKSpGEMMFunction._forward_v1(ctx, graph_indices, graph_values, a3, a4, *rest)
+        ctx.n_inputs = 4 + len(rest)  # backward returns one grad per apply() argument
+        return out
+
+    # ---- v1: dense input + int k ------------------------------------------------
+    @staticmethod
+    def _forward_v1(ctx, graph_indices, graph_values, input_features, k_value,
+                    warp4_metadata=None, num_warps=0, graph_indptr=None, in_degrees=None,
+                    out_degrees=None, graph_indices_T=None, graph_values_T=None):
+        x = _f32(input_features)
+        V, D = x.shape
+        k = int(k_value)
+        if k < D:
+            sparse_data, sparse_selector = maxk_cuda_kernels.topk_cbsr(x, k)
+        else:  # k >= D: all features, identity selector (maxk_spgemm_function.py:58-63)
+            k = D
+            sparse_data = x
+            sparse_selector = torch.arange(D, device=x.device, dtype=torch.uint8) \
+                .unsqueeze(0).expand(V, -1).contiguous()
+        indptr = _indptr_for(graph_indptr, warp4_metadata, num_warps, V)
+        row_div = _f32(in_degrees)
+        out = maxk_cuda_kernels.spgemm_forward(indptr, graph_indices, _f32(graph_values),
+                                               sparse_data, sparse_selector, D, row_div=row_div)
+        ctx.shape_v1 = (V, D)
+        ctx.save_for_backward(indptr, graph_indices, graph_values, sparse_selector,
+                              row_div if row_div is not None else torch.empty(0))
+        ctx.has_div = row_div is not None
+        ctx.mode = "v1"
+        return out
+
+    # ---- v4: precomputed top-k + degrees ---------------------------------------------
+    @staticmethod
+    def _forward_v4(ctx, graph_indices, graph_values, topk_values, topk_indices,
+                    warp4_metadata=None, num_warps=0, graph_indptr=None, degrees=None,
+                    dim_origin=None):
+        vals = _f32(topk_values)
+        sel = topk_indices if topk_indices.dtype == torch.uint8 else topk_indices.to(torch.uint8)
+        sel = sel.contiguous()
+        V, k = vals.shape
+        D = int(dim_origin) if dim_origin is not None else FULL_DIM
+        indptr = _indptr_for(graph_indptr, warp4_metadata, num_warps, V)
+        row_div = _f32(degrees)
+        out = maxk_cuda_kernels.spgemm_forward(indptr, graph_indices, _f32(graph_values), vals,
+                                               sel, D, row_div=row_div)
+        ctx.save_for_backward(indptr, graph_indices, graph_values, sel,
+                              row_div if row_div is not None else torch.empty(0))
+        ctx.has_div = row_div is not None
+        ctx.mode = "v4"
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        indptr, graph_indices, graph_values, sel, row_div = ctx.saved_tensors
+        row_div = row_div if ctx.has_div else None
+        g = grad_output.contiguous()
+        if g.dtype != torch.float32:
+            g = g.float()
+        grad_sparse = maxk_cuda_kernels.sspmm_backward(indptr, graph_indices, _f32(graph_values),
+                                                       g, sel, row_div=row_div)
+        grads = [None] * ctx.n_inputs
+        if ctx.mode == "v1":
+            V, D = ctx.shape_v1
+            if ctx.needs_input_grad[2]:
+                grads[2] = maxk_cuda_kernels.cbsr_scatter_dense(grad_sparse, sel, D)
+        else:
+            grads[2] = grad_sparse
+        return tuple(grads)
+
+
+def maxk_spgemm(graph_indices, graph_values, a3, a4, *rest, **kw):
+    """Both shapes (see module doc):
+    v1: maxk_spgemm(graph_indices, graph_values, input_features, k_value, warp4_metadata=None,
+                    num_warps=0, graph_indptr=None, in_degrees=None, out_degrees=None,
+                    graph_indices_T=None, graph_values_T=None)
+    v4: maxk_spgemm(graph_indices, graph_values, topk_values, topk_indices, warp4_metadata,
+                    num_warps, graph_indptr, degrees, dim_origin=None)"""
+    _require_kernels()
+    if isinstance(a4, torch.Tensor):
+        names = ("warp4_metadata", "num_warps", "graph_indptr", "degrees", "dim_origin")
+        defaults = (None, 0, None, None, None)
+    else:
+        names = ("warp4_metadata", "num_warps", "graph_indptr", "in_degrees", "out_degrees",
+                 "graph_indices_T", "graph_values_T")
+        defaults = (None, 0, None, None, None, None, None)
+    args = list(rest) + [None] * (len(names) - len(rest))
+    for i, n in enumerate(names):
+        if n in kw:
+            args[i] = kw.pop(n)
+        elif i >= len(rest):
+            args[i] = defaults[i]
+    if kw:
+        raise TypeError(f"unexpected keyword arguments: {sorted(kw)}")
+    if isinstance(a4, torch.Tensor) and args[-1] is None:
+        args = args[:-1]
+    return MaxKSpGEMMFunction.apply(graph_indices, graph_values, a3, a4, *args)
+
+
+class MaxKSpmmWrapper:
+    """Holds the warp4 metadata of one graph (maxk_spgemm_function.py:214-267)."""
+
+    def __init__(self, graph_name: str = "", num_warps: int = 12, warp_max_nz: int = 64):
+        self.graph_name = graph_name
+        self.warp4_metadata = None
+        self.num_warps = 0
+        self.num_warps_config = num_warps
+        self.warp_max_nz = warp_max_nz
+        self._indptr_cache = None
+
+    def load_metadata(self, graph_name: Optional[str] = None) -> bool:
+        """Read kernels/w12_nz64_warp_4/<graph>.warp4 (CWD-relative); False on failure."""
+        if graph_name is None:
+            graph_name = self.graph_name
+        if not MAXK_KERNELS_AVAILABLE:
+            print("MaxK kernels not available")
+            return False
+        try:
+            self.warp4_metadata = maxk_cuda_kernels.load_warp4_metadata(
+                graph_name, self.num_warps_config, self.warp_max_nz)
+        except Exception as e:  # noqa: BLE001 -- reference contract: report and return False
+            print(f"Failed to load MaxK metadata: {e}")
+            return False
+        self.num_warps = self.warp4_metadata.size(0) // 4
+        self._indptr_cache = None
+        return True
+
+    def build_metadata(self, graph_indptr: torch.Tensor) -> bool:
+        """Build the warp4 schedule on the GPU from the CSR row pointer (no .warp4 file needed)."""
+        _require_kernels()
+        ip = graph_indptr if graph_indptr.dtype == torch.int32 else graph_indptr.int()
+        self.warp4_metadata = maxk_cuda_kernels.build_warp4_metadata(ip.contiguous(),
+                                                                     self.warp_max_nz)
+        self.num_warps = self.warp4_metadata.size(0) // 4
+        self._indptr_cache = ip.contiguous()
+        return True
+
+    def _indptr(self, graph_indptr, num_v):
+        if graph_indptr is not None:
+            return graph_indptr
+        if self._indptr_cache is None or self._indptr_cache.numel() != num_v + 1:
+            self._indptr_cache = _indptr_for(None, self.warp4_metadata, self.num_warps, num_v)
+        return self._indptr_cache
+
+    def spmm(self, graph_indices, graph_values, a3, a4, *rest, **kw):
+        """v1: spmm(graph_indices, graph_values, input_features, k_value, graph_indptr=None,
+                    in_degrees=None, out_degrees=None, graph_indices_T=None, graph_values_T=None)
+        v4: spmm(graph_indices, graph_values, topk_values, topk_indices, graph_indptr, degrees)"""
+        if isinstance(a4, torch.Tensor):
+            names = ("graph_indptr", "degrees", "dim_origin")
+        else:
+            names = ("graph_indptr", "in_degrees", "out_degrees", "graph_indices_T",
+                     "graph_values_T")
+        vals = dict(zip(names, rest))
+        vals.update(kw)
+        ip = self._indptr(vals.get("graph_indptr"), a3.shape[0])
+        if isinstance(a4, torch.Tensor):
+            return maxk_spgemm(graph_indices, graph_values, a3, a4, self.warp4_metadata,
+                               self.num_warps, ip, vals.get("degrees"),
+                               dim_origin=vals.get("dim_origin"))
+        return maxk_spgemm(graph_indices, graph_values, a3, a4, self.warp4_metadata,
+                           self.num_warps, ip, vals.get("in_degrees"), vals.get("out_degrees"),
+                           vals.get("graph_indices_T"), vals.get("graph_values_T"))

@@ -1,0 +1,101 @@
+"""CPU: the C-ABI library loads, exports every symbol include/maxk_hip.h declares,
+validates arguments on the host, and the Python surfaces refuse to compute
+without a GPU (no fallback).  No kernel is launched here."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "maxk_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(maxk_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_path():
+    syms = declared_symbols()
+    for s in ("maxk_spgemm_forward", "maxk_sspmm_backward", "maxk_topk_cbsr",
+              "maxk_warp4_build", "maxk_warp4_to_row_ptr", "maxk_cbsr_scatter_dense",
+              "maxk_dense_spmm_run", "maxk_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(os.path.join(PKG, "lib", "libmaxk_hip.so"))
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_every_symbol():
+    from maxk_cuda_kernels import _capi
+    assert set(_capi.SIGNATURES) == set(declared_symbols())
+
+
+def test_version_and_device_probe():
+    import maxk_cuda_kernels as mk
+    assert mk.version() == 100
+    assert mk.device_count() >= 0  # 0 here (no GPU); never raises
+
+
+def test_host_side_argument_validation():
+    from maxk_cuda_kernels import _capi
+    L = _capi.load()
+    # k > D, D > 256, negative sizes: rejected before any HIP call
+    assert L.maxk_spgemm_forward(None, None, None, None, None, None, None, 10, 10, 0, 64, 65, 0,
+                                 None, 0, None) == -1
+    assert b"dim_k" in L.maxk_last_error()
+    assert L.maxk_spgemm_forward(None, None, None, None, None, None, None, 10, 10, 0, 257, 16, 0,
+                                 None, 0, None) == -1
+    assert L.maxk_sspmm_backward(None, None, None, None, None, None, None, -1, 10, 0, 64, 16, 0,
+                                 None, 0, None) == -1
+    assert L.maxk_topk_cbsr(None, 64, None, None, None, 10, 64, 0, None) == -1
+    assert L.maxk_topk_cbsr(None, 32, None, None, None, 10, 64, 8, None) == -1  # ld_x < D
+    # forward needs a workspace when rows exist
+    assert L.maxk_spgemm_forward(ctypes.c_void_p(16), None, None, None, None, None,
+                                 ctypes.c_void_p(16), 10, 10, 0, 64, 16, 0, None, 0, None) == -1
+    assert b"workspace" in L.maxk_last_error()
+    # empty problems are valid no-ops
+    assert L.maxk_spgemm_forward(None, None, None, None, None, None, None, 0, 0, 0, 64, 16, 0,
+                                 None, 0, None) == 0
+    assert L.maxk_last_error() == b""
+
+
+def test_workspace_sizes():
+    from maxk_cuda_kernels import _capi
+    L = _capi.load()
+    # slabs: one D-row per work item + a row id per item
+    n = L.maxk_spgemm_forward_workspace_size(1000, 100000, 256, 16, 512)
+    items = -(-101000 // 512)
+    assert n >= items * (256 * 4 + 4)
+    assert L.maxk_spgemm_forward_workspace_size(0, 0, 256, 16, 0) > 0  # one item minimum
+    assert L.maxk_warp4_build_workspace_size(1000) >= 2 * 4000
+
+
+def test_binding_refuses_cpu_tensors():
+    import maxk_cuda_kernels as mk
+    x = torch.zeros(4, 8)
+    with pytest.raises(RuntimeError, match="CUDA"):
+        mk.topk_cbsr(x, 2)
+    ip = torch.zeros(5, dtype=torch.int32)
+    with pytest.raises(RuntimeError, match="CUDA"):
+        mk.spgemm_forward(ip, torch.zeros(0, dtype=torch.int32), torch.zeros(0),
+                          torch.zeros(4, 2), torch.zeros(4, 2, dtype=torch.uint8), 8)
+
+
+def test_autograd_surface_no_cpu_fallback():
+    import maxk_spgemm_function as F
+    assert F.MAXK_KERNELS_AVAILABLE is True
+    ip = torch.tensor([0, 1, 2], dtype=torch.int32)
+    idx = torch.tensor([1, 0], dtype=torch.int32)
+    val = torch.ones(2)
+    x = torch.randn(2, 8, requires_grad=True)
+    with pytest.raises(RuntimeError):
+        F.maxk_spgemm(idx, val, x, 2, graph_indptr=ip)
+    w = F.MaxKSpmmWrapper("does_not_exist")
+    assert w.load_metadata() is False  # reference contract: report and return False

@@ -1,0 +1,83 @@
+"""CPU: the oracle (oracle/maxk_oracle.c) against the reference's own outputs.
+
+Pins the restatement before anything is compared with it: tests/golden/*.npz
+were produced by the reference's maxk_spgemm_function (forward + autograd
+gradient) and generate_meta_csc (warp4) -- see tests/golden/make_golden.py.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import golden_cases, load_golden
+
+CASES = golden_cases()
+TOL = 1e-4  # |a - b| <= TOL * max(1, |ref|)  (north_star: 1e-4 fp32)
+
+
+def close(a, ref, tol=TOL):
+    err = np.abs(a.astype(np.float64) - ref.astype(np.float64))
+    return bool(np.all(err <= tol * np.maximum(1.0, np.abs(ref))))
+
+
+def test_golden_present():
+    assert len(CASES) >= 8
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: p.split("/")[-1][:-4])
+def test_topk_matches_torch_topk(path):
+    z = load_golden(path)
+    v, i = O.topk(z["x"], int(z["k"]))
+    assert np.array_equal(i, z["topk_idx"])
+    assert np.array_equal(v, z["topk_val"])
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: p.split("/")[-1][:-4])
+def test_forward_matches_reference(path):
+    z = load_golden(path)
+    y = O.spgemm_fwd(z["row_ptr"], z["col_idx"], z["val"], z["topk_val"], z["topk_idx"],
+                     int(z["D"]), row_div=z["deg"])
+    assert close(y, z["y_ref"])
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: p.split("/")[-1][:-4])
+def test_backward_matches_reference_autograd(path):
+    z = load_golden(path)
+    gs = O.sspmm_bwd(z["row_ptr"], z["col_idx"], z["val"], z["g"], z["topk_idx"], row_div=z["deg"])
+    assert close(gs, z["grad_cbsr_ref"])
+    tp, ts, tv = O.transpose_csr(z["row_ptr"], z["col_idx"], z["val"])
+    gp = O.sspmm_bwd_pull(tp, ts, tv, z["g"], z["topk_idx"], row_div=z["deg"])
+    assert close(gp, gs, 1e-6)
+    dense = O.scatter_dense(gs, z["topk_idx"], int(z["D"]))
+    assert np.array_equal(np.take_along_axis(dense, z["topk_idx"].astype(np.int64), 1), gs)
+    assert np.count_nonzero(dense) <= gs.size
+
+
+@pytest.mark.parametrize("path", CASES, ids=lambda p: p.split("/")[-1][:-4])
+def test_warp4_matches_reference(path):
+    z = load_golden(path)
+    assert np.array_equal(O.warp4(z["row_ptr"], 64), z["warp4_ref"])
+
+
+def test_oracle_adjoint_identity():
+    """<A.scatter(v), G> == <v, gather(A^T G)>: forward and backward are adjoint."""
+    z = load_golden(CASES[0])
+    rng = np.random.default_rng(3)
+    k, D = int(z["k"]), int(z["D"])
+    V = z["row_ptr"].size - 1
+    v = rng.standard_normal((V, k)).astype(np.float32)
+    g = rng.standard_normal((V, D)).astype(np.float32)
+    y = O.spgemm_fwd(z["row_ptr"], z["col_idx"], z["val"], v, z["topk_idx"], D)
+    gs = O.sspmm_bwd(z["row_ptr"], z["col_idx"], z["val"], g, z["topk_idx"])
+    a = float(np.dot(y.ravel().astype(np.float64), g.ravel()))
+    b = float(np.dot(v.ravel().astype(np.float64), gs.ravel()))
+    assert abs(a - b) <= 1e-4 * max(1.0, abs(a))
+
+
+def test_oracle_row_range_sample():
+    z = load_golden(CASES[0])
+    D = int(z["D"])
+    full = O.spgemm_fwd(z["row_ptr"], z["col_idx"], z["val"], z["topk_val"], z["topk_idx"], D)
+    part = O.spgemm_fwd(z["row_ptr"], z["col_idx"], z["val"], z["topk_val"], z["topk_idx"], D,
+                        rows=(10, 50))
+    assert np.array_equal(part[10:50], full[10:50])
+    assert not part[:10].any() and not part[50:].any()

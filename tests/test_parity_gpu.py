@@ -1,0 +1,339 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+outputs and the pinned CPU oracle.
+
+Tolerances: fp32 outputs |hip - ref| <= 1e-4 * max(1, |ref|) (north_star);
+index vectors (top-k selectors, warp4, row_ptr) bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import golden_cases, load_golden
+
+pytestmark = pytest.mark.gpu
+
+CASES = golden_cases()
+IDS = [p.split("/")[-1][:-4] for p in CASES]
+TOL = 1e-4
+
+
+def close(a, ref, tol=TOL):
+    a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a
+    err = np.abs(a.astype(np.float64) - ref.astype(np.float64))
+    bound = tol * np.maximum(1.0, np.abs(ref.astype(np.float64)))
+    bad = err > bound
+    assert not bad.any(), f"{bad.sum()} elements off; max err {err.max():.3e}"
+    return True
+
+
+def T(a, dev, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return t if dtype is None else t.to(dtype)
+
+
+@pytest.fixture(scope="module")
+def mk(cuda):
+    import maxk_cuda_kernels
+    return maxk_cuda_kernels
+
+
+@pytest.fixture(scope="module")
+def F(cuda):
+    import maxk_spgemm_function
+    assert maxk_spgemm_function.MAXK_KERNELS_AVAILABLE
+    return maxk_spgemm_function
+
+
+# --------------------------------------------------------------------------- golden
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_topk_bit_exact(mk, cuda, path):
+    z = load_golden(path)
+    v, i, i32 = mk.topk_cbsr(T(z["x"], cuda), int(z["k"]), with_int32=True)
+    assert np.array_equal(i.cpu().numpy(), z["topk_idx"])
+    assert np.array_equal(i32.cpu().numpy(), z["topk_idx"].astype(np.int32))
+    assert np.array_equal(v.cpu().numpy(), z["topk_val"])
+
+
+@pytest.mark.parametrize("chunk", [0, 5, 37, 300])
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_forward_golden(mk, cuda, path, chunk):
+    z = load_golden(path)
+    y = mk.spgemm_forward(T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda),
+                          T(z["topk_val"], cuda), T(z["topk_idx"], cuda), int(z["D"]),
+                          row_div=T(z["deg"], cuda), chunk=chunk)
+    close(y, z["y_ref"])
+
+
+@pytest.mark.parametrize("chunk", [0, 5, 37, 300])
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_backward_golden(mk, cuda, path, chunk):
+    z = load_golden(path)
+    gs = mk.sspmm_backward(T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda),
+                           T(z["g"], cuda), T(z["topk_idx"], cuda), row_div=T(z["deg"], cuda),
+                           chunk=chunk)
+    close(gs, z["grad_cbsr_ref"])
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_warp4_build_and_inverse(mk, cuda, path):
+    z = load_golden(path)
+    ip = T(z["row_ptr"], cuda)
+    w4 = mk.build_warp4_metadata(ip, 64)
+    assert np.array_equal(w4.cpu().numpy(), z["warp4_ref"])
+    back = mk.warp4_to_indptr(w4, z["row_ptr"].size - 1)
+    assert np.array_equal(back.cpu().numpy(), z["row_ptr"])
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_reference_binding_signatures(mk, cuda, path):
+    """spmm_maxk_forward/backward(warp4, ...) exactly as the reference callers use them."""
+    z = load_golden(path)
+    V, k, D = z["row_ptr"].size - 1, int(z["k"]), int(z["D"])
+    w4 = T(z["warp4_ref"], cuda)
+    idx, val = T(z["col_idx"], cuda), T(z["val"], cuda)
+    sel = T(z["topk_idx"], cuda)
+    raw = mk.spmm_maxk_forward(w4, idx, val, T(z["topk_val"], cuda), sel, w4.numel() // 4, k,
+                               dim_origin=D)
+    deg = T(z["deg"], cuda)
+    close(raw / deg.unsqueeze(-1), z["y_ref"])
+    g = T(z["g"], cuda)
+    gs = mk.spmm_maxk_backward(w4, idx, val, g / deg.unsqueeze(-1), sel, w4.numel() // 4, k)
+    close(gs, z["grad_cbsr_ref"])
+    if D == 256:  # the reference binding's default output width
+        assert mk.spmm_maxk_forward(w4, idx, val, T(z["topk_val"], cuda), sel, w4.numel() // 4,
+                                    k).shape == (V, 256)
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_autograd_v1_golden(F, cuda, path):
+    z = load_golden(path)
+    x = T(z["x"], cuda).requires_grad_(True)
+    y = F.maxk_spgemm(T(z["col_idx"], cuda), T(z["val"], cuda), x, int(z["k"]),
+                      graph_indptr=T(z["row_ptr"], cuda), in_degrees=T(z["deg"], cuda),
+                      out_degrees=T(z["deg"], cuda))
+    close(y, z["y_ref"])
+    y.backward(T(z["g"], cuda))
+    ref = O.scatter_dense(z["grad_cbsr_ref"], z["topk_idx"], int(z["D"]))
+    close(x.grad, ref)
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_autograd_v4_wrapper_golden(F, cuda, path):
+    z = load_golden(path)
+    ip = T(z["row_ptr"], cuda)
+    w = F.MaxKSpmmWrapper("golden")
+    assert w.build_metadata(ip)
+    tv = T(z["topk_val"], cuda).requires_grad_(True)
+    ti = T(z["topk_idx"], cuda, torch.int64)
+    y = w.spmm(T(z["col_idx"], cuda), T(z["val"], cuda), tv, ti, ip, T(z["deg"], cuda),
+               dim_origin=int(z["D"]))
+    close(y, z["y_ref"])
+    y.backward(T(z["g"], cuda))
+    close(tv.grad, z["grad_cbsr_ref"])
+
+
+# --------------------------------------------------------------------------- oracle, edge cases
+def rand_graph(rng, V, avg, hubs=(), empty=0, cols=None):
+    cols = V if cols is None else cols
+    deg = rng.poisson(avg, V).astype(np.int64)
+    for r, d in hubs:
+        deg[r] = d
+    if empty:
+        deg[rng.choice(V, empty, replace=False)] = 0
+    rows = []
+    for r in range(V):
+        d = min(int(deg[r]), cols)
+        rows.append(np.sort(rng.choice(cols, d, replace=False)) if d else np.zeros(0, np.int64))
+    row_ptr = np.zeros(V + 1, np.int64)
+    np.cumsum([len(x) for x in rows], out=row_ptr[1:])
+    col = np.concatenate(rows) if row_ptr[-1] else np.zeros(0, np.int64)
+    return row_ptr.astype(np.int32), col.astype(np.int32)
+
+
+def run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div=None, chunk=0):
+    y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
+                          D, row_div=None if div is None else T(div, cuda), chunk=chunk)
+    gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda),
+                           row_div=None if div is None else T(div, cuda), chunk=chunk)
+    yo = O.spgemm_fwd(row_ptr, col, val, cv, ci, D, row_div=div)
+    go = O.sspmm_bwd(row_ptr, col, val, g, ci, row_div=div)
+    return y, yo, gs, go
+
+
+@pytest.mark.parametrize("k,D", [(1, 64), (2, 64), (3, 64), (8, 256), (16, 256), (24, 256),
+                                 (32, 256), (48, 256), (64, 256), (96, 256), (128, 256),
+                                 (255, 256), (256, 256), (16, 100), (7, 9)])
+def test_all_k_against_oracle(mk, cuda, k, D):
+    rng = np.random.default_rng(k * 1000 + D)
+    V = 600
+    row_ptr, col = rand_graph(rng, V, 12, hubs=((3, 590), (100, 200)), empty=20)
+    val = rng.random(col.size, dtype=np.float32)
+    x = rng.standard_normal((V, D), dtype=np.float32)
+    cv, ci = O.topk(x, k)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+    for chunk in (0, 13):
+        y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, chunk)
+        close(y, yo)
+        close(gs, go)
+    v, i = mk.topk_cbsr(T(x, cuda), k)
+    assert np.array_equal(i.cpu().numpy(), ci) and np.array_equal(v.cpu().numpy(), cv)
+
+
+def test_empty_graph_and_empty_rows(mk, cuda):
+    D, k, V = 64, 16, 50
+    rng = np.random.default_rng(1)
+    cv = rng.random((V, k), dtype=np.float32)
+    ci = np.stack([rng.choice(D, k, replace=False) for _ in range(V)]).astype(np.uint8)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    row_ptr = np.zeros(V + 1, np.int32)
+    col = np.zeros(0, np.int32)
+    val = np.zeros(0, np.float32)
+    y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D)
+    assert not y.cpu().numpy().any() and not gs.cpu().numpy().any()
+    # only the last row has edges; many leading empty rows share work items
+    row_ptr = np.zeros(V + 1, np.int32)
+    row_ptr[-1] = 3
+    col = np.array([0, 5, 49], np.int32)
+    val = np.array([1.0, 2.0, 3.0], np.float32)
+    for chunk in (0, 1, 2, 7):
+        y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=chunk)
+        close(y, yo)
+        close(gs, go)
+
+
+def test_output_fully_overwritten(mk, cuda):
+    """No zero-init contract: pre-filled output buffers must be overwritten everywhere."""
+    rng = np.random.default_rng(5)
+    V, D, k = 300, 256, 16
+    row_ptr, col = rand_graph(rng, V, 8, empty=30)
+    val = rng.random(col.size, dtype=np.float32)
+    cv, ci = O.topk(rng.standard_normal((V, D), dtype=np.float32), k)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    out = torch.full((V, D), float("nan"), device=cuda)
+    y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
+                          D, out=out, chunk=9)
+    close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, D))
+    gout = torch.full((V, k), float("nan"), device=cuda)
+    gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda),
+                           out=gout)
+    close(gs, O.sspmm_bwd(row_ptr, col, val, g, ci))
+
+
+def test_duplicate_selectors_accumulate(mk, cuda):
+    """Selectors with repeated columns (the reference's random test harness produces them):
+    the kernels accumulate, like the reference's shared-memory sum."""
+    rng = np.random.default_rng(9)
+    V, D, k = 200, 64, 16
+    row_ptr, col = rand_graph(rng, V, 20)
+    val = rng.random(col.size, dtype=np.float32)
+    cv = rng.random((V, k), dtype=np.float32)
+    ci = rng.integers(0, 8, (V, k)).astype(np.uint8)  # heavy duplication
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=17)
+    close(y, yo)
+    close(gs, go)
+
+
+def test_rectangular_shard(mk, cuda):
+    """num_rows != num_cols: a vertex-range shard's rows against the full CBSR."""
+    rng = np.random.default_rng(11)
+    R, C, D, k = 150, 700, 256, 32
+    row_ptr, col = rand_graph(rng, R, 40, cols=C)
+    val = rng.random(col.size, dtype=np.float32)
+    cv, ci = O.topk(rng.standard_normal((C, D), dtype=np.float32), k)
+    g = rng.standard_normal((R, D), dtype=np.float32)
+    y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=64)
+    assert y.shape == (R, D) and gs.shape == (C, k)
+    close(y, yo)
+    close(gs, go)
+
+
+def test_topk_ties_nan_and_uint8(mk, cuda):
+    x = torch.tensor([[1.0, 3.0, 3.0, 2.0, float("nan"), 3.0, -1.0, 0.0]], device=cuda)
+    v, i = mk.topk_cbsr(x, 4)
+    assert i.cpu().tolist() == [[4, 1, 2, 5]]  # NaN largest; ties by ascending column
+    assert torch.isnan(v[0, 0]) and v[0, 1:].cpu().tolist() == [3.0, 3.0, 3.0]
+    rng = np.random.default_rng(2)
+    xu = rng.integers(0, 256, (300, 256)).astype(np.uint8)
+    vu, iu = mk.cuda_topk_maxk(T(xu, cuda), 32)
+    order = np.lexsort((np.tile(np.arange(256), (300, 1)), -xu.astype(np.int32)), axis=1)[:, :32]
+    assert np.array_equal(iu.cpu().numpy(), order.astype(np.uint8))
+    assert np.array_equal(vu.cpu().numpy(), np.take_along_axis(xu, order, 1))
+
+
+def test_scatter_dense_and_selector_gen(mk, cuda):
+    rng = np.random.default_rng(4)
+    cv, ci = O.topk(rng.standard_normal((100, 256), dtype=np.float32), 16)
+    d = mk.cbsr_scatter_dense(T(cv, cuda), T(ci, cuda), 256)
+    assert np.array_equal(d.cpu().numpy(), O.scatter_dense(cv, ci, 256))
+    sel = mk.generate_sparse_selector(1000, 256, 32)
+    s = sel.cpu().numpy().astype(np.int64)
+    assert s.shape == (1000, 32)
+    assert all(len(set(r)) == 32 for r in s)
+
+
+def test_rocsparse_baseline_matches_oracle(mk, cuda):
+    rng = np.random.default_rng(6)
+    V, D, k = 500, 256, 16
+    row_ptr, col = rand_graph(rng, V, 30)
+    val = rng.random(col.size, dtype=np.float32)
+    cv, ci = O.topk(rng.standard_normal((V, D), dtype=np.float32), k)
+    dense = O.scatter_dense(cv, ci, D)
+    y = mk.cusparse_spmm(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(dense, cuda))
+    close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, D))
+
+
+def test_runs_on_current_stream(mk, cuda):
+    rng = np.random.default_rng(8)
+    z = load_golden(CASES[0])
+    s = torch.cuda.Stream()
+    args = [T(z[n], cuda) for n in ("row_ptr", "col_idx", "val", "topk_val", "topk_idx")]
+    with torch.cuda.stream(s):
+        y = mk.spgemm_forward(*args, int(z["D"]), row_div=T(z["deg"], cuda))
+    s.synchronize()
+    close(y, z["y_ref"])
+
+
+def test_hipgraph_capture(mk, cuda):
+    """The launch path allocates/synchronises nothing: it can be captured and replayed."""
+    z = load_golden(CASES[2])
+    args = [T(z[n], cuda) for n in ("row_ptr", "col_idx", "val", "topk_val", "topk_idx")]
+    deg = T(z["deg"], cuda)
+    out = torch.empty(z["row_ptr"].size - 1, int(z["D"]), device=cuda)
+    mk.spgemm_forward(*args, int(z["D"]), row_div=deg, out=out)  # warm up allocator
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        mk.spgemm_forward(*args, int(z["D"]), row_div=deg, out=out, validate=False)
+    out.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    close(out, z["y_ref"])
+
+
+# --------------------------------------------------------------------------- size-independent
+def test_adjoint_identity_large(mk, cuda):
+    """<fwd(v), G> == <v, bwd(G)> on a 2M-edge power-law graph (no oracle needed)."""
+    torch.manual_seed(0)
+    V, E, D, k = 60000, 2_000_000, 256, 16
+    w = torch.arange(1, V + 1, device=cuda, dtype=torch.float32).pow(-0.6)
+    src = torch.multinomial(w, E, replacement=True)
+    dst = torch.randint(0, V, (E,), device=cuda)
+    key = torch.unique(src.long() * V + dst.long())
+    src, dst = (key // V).int(), (key % V).int()
+    row_ptr = torch.zeros(V + 1, dtype=torch.int32, device=cuda)
+    row_ptr[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0).int()
+    val = torch.rand(dst.numel(), device=cuda)
+    v = torch.randn(V, k, device=cuda)
+    sel = mk.generate_sparse_selector(V, D, k)
+    G = torch.randn(V, D, device=cuda)
+    y = mk.spgemm_forward(row_ptr, dst, val, v, sel, D)
+    gs = mk.sspmm_backward(row_ptr, dst, val, G, sel)
+    a = (y.double() * G.double()).sum().item()
+    b = (v.double() * gs.double()).sum().item()
+    assert abs(a - b) <= 1e-4 * max(1.0, abs(a))
+    # row sums: sum_j Y[r, j] == A . (sum_l v[c, l])
+    rs = torch.sparse_csr_tensor(row_ptr.long(), dst.long(), val, (V, V)) @ v.sum(1, keepdim=True)
+    assert torch.allclose(y.sum(1), rs[:, 0], rtol=1e-4, atol=1e-3)
