@@ -1,0 +1,358 @@
+#!/usr/bin/env python3
+"""Benchmark of the MaxK-GNN aggregation hot path on MI355X.
+
+One step = forward SpGEMM (CSR adjacency x CBSR top-k features -> dense) +
+backward SSpMM (dense grad -> CBSR-shaped grad) over the whole graph, the two
+kernels the reference times in kernels/main.cu:163-172.
+
+Metric (BASELINE.json): SpGEMM+SSpMM GTEPS = 2E / (t_fwd + t_bwd) / 1e9,
+whole job, inputs resident in HBM before the timed region.  Default workload:
+synthetic Reddit-sized graph (V=232,965, E=114,615,891, symmetric power-law with
+self loops), hidden D=256, k=16 -- BASELINE.json configs[1] at k=16.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--graph reddit] [--k 16]
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): vertex-range
+shards balanced by nnz; per step an RCCL all-gather of the CBSR rows before the
+forward and a reduce-scatter of the CBSR-gradient partials after the backward
+(strong scaling: the graph is fixed).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "spgemm-prunning_amd"))
+
+METRIC = "SpGEMM+SSpMM GTEPS (edges/s) & HBM-BW% on Reddit h=256 k=16; vs CPU SpMM"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+# name: V, E (published sizes), power-law (alpha, offset) fitted so
+# the max/avg degree ratio resembles the real graph
+PRESETS = {
+    "reddit": dict(V=232_965, E=114_615_891, alpha=0.7, i0=200, D=256, k=16),
+    "products": dict(V=2_449_029, E=123_718_280, alpha=0.75, i0=3000, D=256, k=32),
+    "proteins": dict(V=132_534, E=79_122_504, alpha=0.45, i0=2000, D=256, k=64),
+    "flickr": dict(V=89_250, E=989_006, alpha=0.9, i0=30, D=64, k=16),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# --------------------------------------------------------------------------- synthetic graph
+def make_graph(V, E, alpha, i0, seed, device):
+    """Symmetric Chung-Lu power-law graph with self loops, deduplicated, CSR with sorted
+    columns (the shape dataset_gen.py:44-115 produces), exactly E edges when E-V is even."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    pairs_target = (E - V) // 2
+    w = (torch.arange(V, device=device, dtype=torch.float64) + i0) ** (-alpha)
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    keys = torch.empty(0, dtype=torch.int64, device=device)
+    need = pairs_target
+    while keys.numel() < pairs_target:
+        m = int(need * 1.25) + 4096
+        a = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device, dtype=torch.float64))
+        b = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device, dtype=torch.float64))
+        a.clamp_(max=V - 1)
+        b.clamp_(max=V - 1)
+        lo, hi = torch.minimum(a, b), torch.maximum(a, b)
+        k = (lo * V + hi)[lo != hi]
+        keys = torch.unique(torch.cat([keys, k]))
+        need = pairs_target - keys.numel()
+        del a, b, lo, hi, k
+    keys = keys[torch.randperm(keys.numel(), generator=g, device=device)[:pairs_target]]
+    relabel = torch.randperm(V, generator=g, device=device)
+    lo, hi = relabel[keys // V], relabel[keys % V]
+    del keys
+    loops = torch.arange(V, device=device)
+    src = torch.cat([lo, hi, loops])
+    dst = torch.cat([hi, lo, loops])
+    del lo, hi
+    key = torch.sort(src * V + dst).values
+    del src, dst
+    src, dst = key // V, key % V
+    row_ptr = torch.zeros(V + 1, dtype=torch.int64, device=device)
+    row_ptr[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)
+    return row_ptr.to(torch.int32), dst.to(torch.int32)
+
+
+def alg_bytes(V, E, D, k, Vc=None):
+    """Algorithmic bytes per launch: row_ptr, col_idx+val, per-edge CBSR
+    gather (k f32 + k u8), dense read/write once; bwd adds the [V,k] gradient write."""
+    Vc = V if Vc is None else Vc
+    fwd = 4 * (V + 1) + 8 * E + 5 * k * E + 4 * V * D
+    bwd = fwd + 4 * Vc * k
+    return fwd, bwd
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
+    """Oracle (port of the reference kernels' semantics, 1 thread) on a row sample sized
+    for ~target_s seconds of CPU work; returns the cpu_baseline JSON object."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.set_num_threads(1)
+    rp = row_ptr.cpu().numpy()
+    c, v = col.cpu().numpy(), val.cpu().numpy()
+    cvn, cin, Gn = cv.cpu().numpy(), ci.cpu().numpy(), G.cpu().numpy()
+    E = int(rp[-1])
+
+    def run(r1):
+        t0 = time.perf_counter()
+        O.spgemm_fwd(rp, c, v, cvn, cin, D, rows=(0, r1))
+        t1 = time.perf_counter()
+        O.sspmm_bwd(rp, c, v, Gn, cin, rows=(0, r1))
+        t2 = time.perf_counter()
+        return t1 - t0, t2 - t1
+
+    # calibrate on ~1% of the edges, then size the sample
+    r_cal = int(np.searchsorted(rp, E // 100))
+    tf, tb = run(r_cal)
+    per_edge = (tf + tb) / max(1, int(rp[r_cal]))
+    e_s = min(E, int(target_s / per_edge))
+    r1 = int(np.searchsorted(rp, e_s))
+    r1 = max(1, min(r1, len(rp) - 1))
+    tf, tb = run(r1)
+    es = int(rp[r1])
+    return {
+        "value": round(2 * es / (tf + tb) / 1e9, 6), "unit": "GTEPS", "cores": 1, "kind": "port",
+        "sample": (f"oracle/maxk_oracle.c fwd SpGEMM + bwd SSpMM (push), 1 thread, rows [0,{r1}) "
+                   f"of the same graph = {es} of {E} edges ({100.0 * es / E:.1f}%); "
+                   f"fwd {tf:.2f}s, bwd {tb:.2f}s"),
+    }
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--graph", default="reddit", choices=sorted(PRESETS))
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--dim", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--chunk", type=int, default=0, help="tokens per work item (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rocsparse", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--bwd-mode", default="csc", choices=["csc", "atomic"])
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import maxk_cuda_kernels as mk
+
+    P = dict(PRESETS[args.graph])
+    D = args.dim or P["D"]
+    k = args.k or P["k"]
+    V = P["V"]
+    E_target = P["E"] - ((P["E"] - V) % 2)
+    t0 = time.time()
+    row_ptr, col = make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
+    E = col.numel()
+    gen = torch.Generator(device=dev).manual_seed(123)  # kernels/main.cu:74-77 seed
+    val = torch.rand(E, generator=gen, device=dev)
+    X = torch.rand(V, D, generator=gen, device=dev)
+    G = torch.rand(V, D, generator=gen, device=dev)
+    deg = torch.diff(row_ptr)
+    if rank == 0:
+        log(f"[bench] graph {args.graph}: V={V} E={E} max_deg={int(deg.max())} "
+            f"avg_deg={E / V:.1f} gen {time.time() - t0:.1f}s")
+
+    # ---- shard by vertex range, balanced by nnz
+    if world > 1:
+        bounds = torch.searchsorted(row_ptr.long(), torch.arange(world + 1, device=dev) * E // world)
+        bounds[0], bounds[-1] = 0, V
+        bnd = bounds.tolist()
+        v0, v1 = bnd[rank], bnd[rank + 1]
+        vmax = max(bnd[i + 1] - bnd[i] for i in range(world))
+        e0, e1 = int(row_ptr[v0]), int(row_ptr[v1])
+        l_row_ptr = (row_ptr[v0:v1 + 1] - e0).contiguous()
+        owner = torch.searchsorted(torch.tensor(bnd[1:], device=dev), col.long()[e0:e1], right=True)
+        l_col = (owner * vmax + (col.long()[e0:e1] - torch.tensor(bnd, device=dev)[owner])).int()
+        l_val = val[e0:e1].contiguous()
+        l_X = X[v0:v1]
+        l_G = G[v0:v1].contiguous()
+        n_cols = world * vmax
+    else:
+        v0, v1, vmax = 0, V, V
+        l_row_ptr, l_col, l_val, l_X, l_G, n_cols = row_ptr, col, val, X, G, V
+    nl = v1 - v0
+    El = l_col.numel()
+
+    # ---- CBSR of the local rows (the MaxK encode), padded to vmax rows for the collectives
+    cv_loc = torch.zeros(vmax, k, device=dev)
+    ci_loc = torch.zeros(vmax, k, dtype=torch.uint8, device=dev)
+    cv_loc[:nl], ci_loc[:nl] = mk.topk_cbsr(l_X, k)
+    if world > 1:
+        cv_all = torch.empty(n_cols, k, device=dev)
+        ci_all = torch.empty(n_cols, k, dtype=torch.uint8, device=dev)
+        gs_all = torch.empty(n_cols, k, device=dev)
+        gs_loc = torch.empty(vmax, k, device=dev)
+    else:
+        cv_all, ci_all = cv_loc, ci_loc
+        gs_all = gs_loc = torch.empty(V, k, device=dev)
+    y = torch.empty(nl, D, device=dev)
+    if world > 1:
+        dist.all_gather_into_tensor(cv_all, cv_loc)
+        dist.all_gather_into_tensor(ci_all, ci_loc)
+    # one validated call (row_ptr/col_idx/selector ranges) before the raw timed launches
+    mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, validate=True)
+    # per-graph setup (like the reference's warp4 files): transpose plan for the backward
+    torch.cuda.synchronize()
+    t_plan = time.perf_counter()
+    plan = mk.transpose_plan(l_col, n_cols) if args.bwd_mode == "csc" else None
+    torch.cuda.synchronize()
+    t_plan = time.perf_counter() - t_plan
+
+    # HIP events on the stream the kernels run on (torch's current stream)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def step(ev=None):
+        if world > 1:
+            dist.all_gather_into_tensor(cv_all, cv_loc)
+            dist.all_gather_into_tensor(ci_all, ci_loc)
+        if ev:
+            ev[0].record()
+        mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, chunk=args.chunk,
+                          validate=False)
+        if ev:
+            ev[1].record()
+        mk.sspmm_backward(l_row_ptr, l_col, l_val, l_G, ci_all, out=gs_all, chunk=args.chunk,
+                          validate=False, mode=args.bwd_mode, plan=plan)
+        if ev:
+            ev[2].record()
+        if world > 1:
+            dist.reduce_scatter_tensor(gs_loc, gs_all)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- sanity: forward/backward adjoint identity on the timed buffers
+    a = (y.double() * l_G.double()).sum()
+    b = (cv_all.double() * gs_all.double()).sum()
+    if dist:
+        ab = torch.stack([a, b])
+        dist.all_reduce(ab)
+        a, b = ab[0], ab[1]
+    adj_err = abs(float(a) - float(b)) / max(1.0, abs(float(a)))
+
+    fwd_ms = [e[0].elapsed_time(e[1]) for e in evs]
+    bwd_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    fwd_avg = float(np.mean(fwd_ms))
+    bwd_avg = float(np.mean(bwd_ms))
+    ms_per_step = 1000.0 * elapsed / args.steps
+    value = 2.0 * E * args.steps / elapsed / 1e9
+    B_f, B_b = alg_bytes(nl, El, D, k, n_cols)
+    kern = "sspmm_bwd_kernel" if bwd_avg >= fwd_avg else "spgemm_fwd_kernel"
+    t_dom, B_dom = (bwd_avg, B_b) if bwd_avg >= fwd_avg else (fwd_avg, B_f)
+    achieved = B_dom / (t_dom * 1e-3) / 1e9
+
+    extra = {
+        "fwd_ms": round(fwd_avg, 4), "bwd_ms": round(bwd_avg, 4),
+        "fwd_gteps": round(El / fwd_avg / 1e6, 3), "bwd_gteps": round(El / bwd_avg / 1e6, 3),
+        "fwd_alg_GBs": round(B_f / fwd_avg / 1e6, 1), "bwd_alg_GBs": round(B_b / bwd_avg / 1e6, 1),
+        "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
+        "bwd_mode": args.bwd_mode, "transpose_plan_s": round(t_plan, 4),
+    }
+
+    if rank == 0 and world == 1:
+        # CBSR encode (top-k) and the dense rocSPARSE SpMM denominator, outside the timed region
+        for _ in range(3):
+            mk.topk_cbsr(X, k)
+        torch.cuda.synchronize()
+        e0_, e1_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0_.record()
+        for _ in range(10):
+            mk.topk_cbsr(X, k)
+        e1_.record()
+        e1_.synchronize()
+        extra["topk_ms"] = round(e0_.elapsed_time(e1_) / 10, 4)
+        if not args.no_rocsparse:
+            dense = mk.cbsr_scatter_dense(cv_all, ci_all, D)
+            plan = mk.DenseSpMMPlan(row_ptr, col, val, dense)
+            for _ in range(3):
+                plan.run()
+            torch.cuda.synchronize()
+            e0_.record()
+            for _ in range(10):
+                plan.run()
+            e1_.record()
+            e1_.synchronize()
+            rs = e0_.elapsed_time(e1_) / 10
+            err = ((plan.y - y).abs() / y.abs().clamp(min=1)).max().item()
+            extra.update({"rocsparse_spmm_ms": round(rs, 4),
+                          "speedup_fwd_vs_rocsparse": round(rs / fwd_avg, 3),
+                          "speedup_bwd_vs_rocsparse": round(rs / bwd_avg, 3),
+                          "rocsparse_vs_maxk_max_rel_err": err})
+            plan.close()
+            del dense
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(row_ptr, col, val, cv_all, ci_all, G, D, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 4), "unit": "GTEPS", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"{args.graph}-synthetic fwd SpGEMM + bwd SSpMM, V={V} E={E} D={D} "
+                             f"k={k}"),
+                "graph": args.graph, "V": V, "E": E, "D": D, "k": k,
+                "parallelism": f"vertex-range x{world}" if world > 1 else "single-gpu",
+            },
+            "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "alg_bytes_per_launch": B_dom,
+                         "launch_ms": round(t_dom, 4)},
+            "cpu_baseline": cpu,
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -48,16 +48,18 @@ int maxk_device_count(void);
  * Forward row-wise-product SpGEMM:  out = diag(1/row_div) . A . scatter(cbsr)
  *   out[r, cbsr_idx[c,l]] += edge_val[e] * cbsr_val[c,l]   (e in row r, c = col_idx[e])
  * Every output row is written (rows without edges get zeros): no zero-init of
- * `out` is needed.  row_div may be NULL (no normalisation).
+ * `out` is needed.  row_div may be NULL (no normalisation).  Duplicate
+ * selectors within a CBSR row accumulate; selectors >= dim_origin are ignored.
  * Replaces: spmm_kernel_opt2_sparse_v3 (kernels/spmm_maxk.cu:17-106),
  *           its launcher spmm_kernel_opt2_sparse_v3_wrapper
  *           (cuda_kernel_wrappers.cu:38-56) and the /in_degrees of
  *           maxk_spgemm_function.py:85-86.
  * chunk_edges: edges per wavefront work item (0 = auto).
- * workspace: >= maxk_spgemm_forward_workspace_size(...) bytes (split-row slabs).
+ * workspace: >= maxk_spgemm_forward_workspace_size(...) bytes, 256-B aligned
+ *            (packed CBSR records + split-row slabs).
  * ------------------------------------------------------------------------- */
-size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t num_e, int32_t dim_origin,
-                                          int32_t dim_k, int32_t chunk_edges);
+size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                          int32_t dim_origin, int32_t dim_k, int32_t chunk_edges);
 int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
                         const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div,
                         float *out, int64_t num_rows, int64_t num_cols, int64_t num_e,
@@ -80,6 +82,32 @@ int maxk_sspmm_backward(const int32_t *row_ptr, const int32_t *col_idx, const fl
                         float *grad_cbsr, int64_t num_rows, int64_t num_cols, int64_t num_e,
                         int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
                         void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Same backward, two-phase and atomic-free (bitwise deterministic): phase 1
+ * stores each edge's k-float contribution in CSR edge order, phase 2 gathers
+ * and sums the contributions of every destination through the CSC permutation.  Needs the transpose plan of the graph
+ * (maxk_transpose_plan) and a workspace of
+ * maxk_sspmm_backward_csc_workspace_size(...) bytes (about num_e*k*4).
+ * ------------------------------------------------------------------------- */
+size_t maxk_sspmm_backward_csc_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                              int32_t dim_origin, int32_t dim_k,
+                                              int32_t chunk_edges);
+int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                            const float *grad_out, const float *row_div, const uint8_t *cbsr_idx,
+                            const int32_t *col_ptr, const int32_t *csc_eid, float *grad_cbsr,
+                            int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                            int32_t dim_k, int32_t chunk_edges, void *workspace,
+                            size_t workspace_bytes, void *stream);
+
+/* Transpose plan of a CSR graph (once per graph): col_ptr[num_cols+1] of the
+ * CSC and csc_eid[num_e] = the CSR edge id held by CSC slot t (stable in CSR order).
+ * Replaces the CSC side files of generate_meta_csc.py:14-93 /
+ * load_warp4_metadata_csc (binding_v2.py:320-351). */
+size_t maxk_transpose_plan_workspace_size(int64_t num_cols, int64_t num_e);
+int maxk_transpose_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
+                        int32_t *col_ptr, int32_t *csc_eid, void *workspace,
+                        size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * CBSR encode (MaxK top-k): per row the k largest of dim_origin values, in

@@ -87,15 +87,18 @@ void oracle_spgemm_fwd(const int32_t *row_ptr, const int32_t *col_idx, const flo
  * maxk_spgemm_function.py:154-155), then for each edge r->c and lane l
  *   gs[c,l] += val[e] * G[r, sel[c,l]]
  * Single-threaded: the push scatters into arbitrary rows, and the sum order is
- * the reference's CSR order.
+ * the reference's CSR order.  num_rows = rows of A / G, num_cols = CBSR rows;
+ * only source rows [r_begin, r_end) are pushed (bounded CPU-baseline samples).
  */
 void oracle_sspmm_bwd(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                       const float *grad, const float *row_div, const uint8_t *cbsr_idx,
-                      float *grad_cbsr, int64_t V, int32_t D, int32_t k)
+                      float *grad_cbsr, int64_t num_rows, int64_t num_cols, int32_t D, int32_t k,
+                      int64_t r_begin, int64_t r_end)
 {
-    double *acc = (double *)calloc((size_t)V * (size_t)k, sizeof(double));
+    (void)num_rows;
+    double *acc = (double *)calloc((size_t)num_cols * (size_t)k, sizeof(double));
     double *g = (double *)malloc(sizeof(double) * (size_t)D);
-    for (int64_t r = 0; r < V; ++r) {
+    for (int64_t r = r_begin; r < r_end; ++r) {
         const float *gr = grad + r * (int64_t)D;
         for (int32_t j = 0; j < D; ++j)
             g[j] = row_div ? (double)gr[j] / (double)row_div[r] : (double)gr[j];
@@ -107,7 +110,7 @@ void oracle_sspmm_bwd(const int32_t *row_ptr, const int32_t *col_idx, const floa
             for (int32_t l = 0; l < k; ++l) a[l] += w * g[sv[l]];
         }
     }
-    for (int64_t i = 0; i < V * (int64_t)k; ++i) grad_cbsr[i] = (float)acc[i];
+    for (int64_t i = 0; i < num_cols * (int64_t)k; ++i) grad_cbsr[i] = (float)acc[i];
     free(g);
     free(acc);
 }

@@ -44,7 +44,7 @@ def lib():
         L.oracle_spgemm_fwd.argtypes = [_i32p, _i32p, _f32p, _f32p, _u8p, ctypes.c_void_p,
                                         _f32p, _i64, _i32, _i32, _i64, _i64]
         L.oracle_sspmm_bwd.argtypes = [_i32p, _i32p, _f32p, _f32p, ctypes.c_void_p, _u8p,
-                                       _f32p, _i64, _i32, _i32]
+                                       _f32p, _i64, _i64, _i32, _i32, _i64, _i64]
         L.oracle_sspmm_bwd_pull.argtypes = [_i32p, _i32p, _f32p, _f32p, ctypes.c_void_p, _u8p,
                                             _f32p, _i64, _i32, _i32, _i64, _i64]
         L.oracle_topk.argtypes = [_f32p, _f32p, _u8p, _i64, _i32, _i32]
@@ -94,16 +94,19 @@ def spgemm_fwd(row_ptr, col_idx, val, cbsr_val, cbsr_idx, D, row_div=None, rows=
     return out
 
 
-def sspmm_bwd(row_ptr, col_idx, val, grad, cbsr_idx, row_div=None):
+def sspmm_bwd(row_ptr, col_idx, val, grad, cbsr_idx, row_div=None, rows=None):
     """Backward SSpMM in the reference's push order, kernels/spmm_maxk_backward.cu:52-103
-    (G / out_deg first, maxk_spgemm_function.py:154-155).  Returns fp32 [V, k]."""
+    (G / out_deg first, maxk_spgemm_function.py:154-155).  Returns fp32 [num_cols, k]
+    (num_cols = rows of cbsr_idx).  ``rows=(r0, r1)`` pushes only those source rows."""
     row_ptr, col_idx, val = _c(row_ptr, np.int32), _c(col_idx, np.int32), _c(val, np.float32)
     grad, cbsr_idx = _c(grad, np.float32), _c(cbsr_idx, np.uint8)
-    V, D = grad.shape
-    k = cbsr_idx.shape[1]
-    out = np.zeros((V, k), dtype=np.float32)
+    R, D = grad.shape
+    C, k = cbsr_idx.shape
+    assert row_ptr.shape[0] == R + 1
+    out = np.zeros((C, k), dtype=np.float32)
     keep, div = _opt_f32(row_div)
-    lib().oracle_sspmm_bwd(row_ptr, col_idx, val, grad, div, cbsr_idx, out, V, D, k)
+    r0, r1 = (0, R) if rows is None else rows
+    lib().oracle_sspmm_bwd(row_ptr, col_idx, val, grad, div, cbsr_idx, out, R, C, D, k, r0, r1)
     del keep
     return out
 

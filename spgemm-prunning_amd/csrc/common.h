@@ -16,6 +16,24 @@ constexpr int kBlock = 256;        // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows are 256 floats
 
+// Tuning knobs (compile-time; tools/tune.sh builds variants).  *_U = edge
+// batches in flight per wave, *_WAVES = __launch_bounds__ min waves per SIMD.
+#ifndef MAXK_FWD_U
+#define MAXK_FWD_U 8
+#endif
+#ifndef MAXK_BWD_U
+#define MAXK_BWD_U 8
+#endif
+#ifndef MAXK_FWD_WAVES
+#define MAXK_FWD_WAVES 1
+#endif
+#ifndef MAXK_BWD_WAVES
+#define MAXK_BWD_WAVES 1
+#endif
+#ifndef MAXK_SUM_U
+#define MAXK_SUM_U 4
+#endif
+
 // ---- error reporting (host) ----
 void set_error(const char *fmt, ...);
 void clear_error();

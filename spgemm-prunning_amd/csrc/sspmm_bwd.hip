@@ -3,48 +3,143 @@
 //
 // Semantics: kernels/spmm_maxk_backward.cu:15-115 (push from the CSR of A, which
 // yields the A^T product) and the /out_degrees of maxk_spgemm_function.py:154-155.
-// Design:
-//  * Same token-stream work partition as the forward (common.h): one wave per
-//    item of C tokens, so hub rows are split and short rows are batched.
-//  * Per row r of the item: the wave stages G[r, :] / row_div[r] into a
-//    256-float LDS row (16-B loads), then walks the row's edges with
-//    KG = pow2ceil(k) lanes per edge: lane l reads sel[c, l] (u8), takes
-//    G_lds[sel] and issues one global fp32 atomic add into grad_cbsr[c, l].
-//    A wave step therefore adds 64/KG contiguous k-float rows -- the
-//    "contiguous segments" atomic shape of the MI355X guide.
-//  * grad_cbsr is zeroed by hipMemsetAsync on the same stream first.
+//
+// The push reads every G row once (staged in LDS, 16-B loads) and produces one
+// k-float contribution per edge that must be summed per destination c.  Two
+// forms of that sum:
+//  * atomic (maxk_sspmm_backward): one global fp32 atomic per (edge, l) into
+//    grad_cbsr (zeroed first).  No preprocessing, but E*k*4 bytes of memory-side
+//    atomics, which MI355X executes at ~1.3 TB/s chip-wide
+//    (MI355X_MICROARCH.md, Global float atomics) -- the kernel sits exactly on
+//    that ceiling (6.2 ms for Reddit-sized k=16).
+//  * two-phase (maxk_sspmm_backward_csc, needs maxk_transpose_plan): phase 1
+//    stores each edge's contribution row in CSR edge order (streaming stores;
+//    scattering them to CSC slots instead measured 4.7 ms, partial-line writes);
+//    phase 2 gathers the rows of each destination through the CSC permutation
+//    and sums them in a fixed order (cross-lane butterflies).  2*E*k*4 bytes of
+//    plain traffic instead of E*k*4 of atomics, and bitwise deterministic.
+// Both use the token-stream work partition of common.h (one wave per item of C
+// tokens, hub rows split, short rows batched).
 #include "common.h"
 
 namespace maxk {
 namespace {
 
-template <int KG, int U>
+enum { kAtomic = 0, kStore = 1 };
+
+// Walk edges [sb, se) (sb < se) of one staged row.  All loads are
+// unconditional (clamped addresses).
+//  kAtomic: one predicated global fp32 atomic per (edge, l).
+//  kStore (k <= KG): contribution rows go to T in CSR edge order with a
+//    one-batch store lag.  On gfx950 stores count in vmcnt with the loads, so a
+//    wait for a load drains every OLDER store: per batch the order is
+//    [prefetch col/val of batch i+1] [selector loads of batch i] [stores of
+//    batch i-1] [wait selectors] -> the stores in flight are always younger than
+//    the loads being waited for.  Masked lanes store to the dummy row of T, so
+//    no store is predicated (a predicated store becomes a branch + full wait).
+template <int KG, int U, int MODE>
 __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__restrict__ col_idx,
                                            const float *__restrict__ edge_val,
                                            const uint8_t *__restrict__ cbsr_idx,
-                                           float *__restrict__ grad_cbsr, int64_t sb, int64_t se,
+                                           float *__restrict__ dst, int dummy, int sb, int se,
                                            int k, int lane) {
     constexpr int G = kWave / KG;
+    constexpr int GU = G * U;
     const int grp = lane / KG;
     const int l0 = lane % KG;
-    for (int64_t base = sb; base < se; base += (int64_t)G * U) {
-        int c[U];
-        float w[U];
+    const int last = se - 1;
+    int c[U];
+    float w[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t e = base + u * G + grp;
-            const bool ok = e < se;
-            c[u] = ok ? col_idx[e] : -1;
-            w[u] = ok ? edge_val[e] : 0.f;
-        }
-        for (int l = l0; l < k; l += KG) {
+    for (int u = 0; u < U; ++u) {
+        const int e = sb + u * G + grp;
+        const int ec = e < se ? e : last;
+        c[u] = col_idx[ec];
+        w[u] = edge_val[ec];
+    }
+    if (MODE == kStore && k <= KG) {
+        const bool lok = l0 < k;
+        const int lc = lok ? l0 : k - 1;
+        float xp[U] = {};
+        int rp[U];  // T row of each pending store (dummy for masked lanes)
+        bool pending = false;
+        for (int base = sb;; base += GU) {
+            const bool has_next = base + GU < se;  // wave-uniform
+            int cn[U];
+            float wn[U];
+            if (has_next) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int e = base + GU + u * G + grp;
+                    const int ec = e < se ? e : last;
+                    cn[u] = col_idx[ec];
+                    wn[u] = edge_val[ec];
+                }
+            }
             int s[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (c[u] >= 0) s[u] = cbsr_idx[c[u] * k + l];
+            for (int u = 0; u < U; ++u) {
+#ifdef MAXK_ABLATE_NOSEL
+                s[u] = (c[u] + lc * 16) & 255;
+#else
+                s[u] = cbsr_idx[c[u] * k + lc];
+#endif
+            }
+#ifndef MAXK_ABLATE_NOSTORE
+            if (pending) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (c[u] >= 0) atomicAdd(&grad_cbsr[c[u] * k + l], w[u] * g_lds[s[u]]);
+                for (int u = 0; u < U; ++u) dst[(size_t)(uint32_t)rp[u] * k + lc] = xp[u];
+            }
+#endif
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = base + u * G + grp;
+#ifdef MAXK_ABLATE_NOSTORE
+                xp[u] += w[u] * g_lds[s[u]];
+#else
+                xp[u] = w[u] * g_lds[s[u]];
+#endif
+                rp[u] = (e < se && lok) ? e : dummy;
+            }
+            pending = true;
+            if (!has_next) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                c[u] = cn[u];
+                w[u] = wn[u];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) dst[(size_t)(uint32_t)rp[u] * k + lc] = xp[u];
+        return;
+    }
+    for (int base = sb;; base += GU) {
+        const bool has_next = base + GU < se;  // wave-uniform
+        for (int lb = 0; lb < k; lb += KG) {
+            const int l = lb + l0;
+            const bool lok = l < k;
+            const int lc = lok ? l : k - 1;
+            int s[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) s[u] = cbsr_idx[c[u] * k + lc];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = base + u * G + grp;
+                const float x = w[u] * g_lds[s[u]];
+                if (MODE == kAtomic) {
+                    if (e < se && lok) atomicAdd(&dst[c[u] * k + l], x);
+                } else {
+                    dst[(size_t)(uint32_t)((e < se && lok) ? e : dummy) * k + (lok ? l : 0)] = x;
+                }
+            }
+        }
+        if (!has_next) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = base + GU + u * G + grp;
+            const int ec = e < se ? e : last;
+            c[u] = col_idx[ec];
+            w[u] = edge_val[ec];
         }
     }
 }
@@ -70,13 +165,12 @@ __device__ __forceinline__ void stage_row(float *g_lds, const float *__restrict_
     wave_lds_fence();
 }
 
-template <int KG, int U>
-__global__ __launch_bounds__(kBlock) void sspmm_bwd_kernel(
+template <int KG, int U, int MODE>
+__global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
     const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
     const float *__restrict__ edge_val, const float *__restrict__ grad,
     const float *__restrict__ row_div, const uint8_t *__restrict__ cbsr_idx,
-    float *__restrict__ grad_cbsr, int num_rows, int64_t num_e, int D, int k, int chunk,
-    int n_items) {
+    float *__restrict__ dst, int num_rows, int64_t num_e, int D, int k, int chunk, int n_items) {
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kMaxDim];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
@@ -97,7 +191,8 @@ __global__ __launch_bounds__(kBlock) void sspmm_bwd_kernel(
         if (sb < se) {
             const float div = row_div ? row_div[r - 1] : 1.f;
             stage_row(g_lds, grad + (int64_t)(r - 1) * D, D, div, row_div != nullptr, lane);
-            push_edges<KG, U>(g_lds, col_idx, edge_val, cbsr_idx, grad_cbsr, sb, se, k, lane);
+            push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)sb,
+                                    (int)se, k, lane);
         }
     }
     for (; r < num_rows; ++r) {
@@ -108,19 +203,130 @@ __global__ __launch_bounds__(kBlock) void sspmm_bwd_kernel(
         if (rb >= se) continue;  // empty row: nothing to push
         const float div = row_div ? row_div[r] : 1.f;
         stage_row(g_lds, grad + (int64_t)r * D, D, div, row_div != nullptr, lane);
-        push_edges<KG, U>(g_lds, col_idx, edge_val, cbsr_idx, grad_cbsr, rb, se, k, lane);
+        push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)rb,
+                                (int)se, k, lane);
     }
 }
 
-template <int KG>
-void launch_bwd(dim3 grid, hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
-                const float *edge_val, const float *grad, const float *row_div,
-                const uint8_t *cbsr_idx, float *grad_cbsr, int num_rows, int64_t num_e, int D,
-                int k, int chunk, int n_items) {
-    constexpr int U = KG >= 8 ? 8 : 4;
-    hipLaunchKernelGGL((sspmm_bwd_kernel<KG, U>), grid, dim3(kBlock), 0, s, row_ptr, col_idx,
-                       edge_val, grad, row_div, cbsr_idx, grad_cbsr, num_rows, num_e, D, k, chunk,
-                       n_items);
+// ---- phase 2: grad_cbsr[c, :] = sum over the CSC slots t of c of T[eid[t], :] -------
+
+// Sum the contribution rows T[eid[t]] (k floats each) for t in [tb, te) into
+// dst[0:k], in a fixed order.  VEC (k in {4,8,...,256}): LR = k/4 lanes per row
+// (16-B loads), 64/LR rows per wave step, U steps in flight; the row groups are
+// combined by xor butterflies.  Scalar: KG = pow2ceil(k) lanes per row.
+template <bool VEC, int KG>
+__device__ __forceinline__ void segment_sum(const float *__restrict__ T,
+                                            const int32_t *__restrict__ eid, int64_t tb,
+                                            int64_t te, int k, float *__restrict__ dst, int lane) {
+    constexpr int U = MAXK_SUM_U;
+    if constexpr (VEC) {
+        const int LR = k / 4, RI = kWave / LR;
+        const int g = lane / LR, q = lane % LR;
+        const float4 *__restrict__ T4 = reinterpret_cast<const float4 *>(T);
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int64_t base = tb; base < te; base += (int64_t)RI * U) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t t = base + u * RI + g;
+                const int e = eid[t < te ? t : tb];
+                v[u] = T4[(size_t)(uint32_t)e * LR + q];
+                if (t >= te) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                a.x += v[u].x;
+                a.y += v[u].y;
+                a.z += v[u].z;
+                a.w += v[u].w;
+            }
+        }
+        for (int off = LR; off < kWave; off <<= 1) {
+            a.x += __shfl_xor(a.x, off);
+            a.y += __shfl_xor(a.y, off);
+            a.z += __shfl_xor(a.z, off);
+            a.w += __shfl_xor(a.w, off);
+        }
+        if (g == 0) reinterpret_cast<float4 *>(dst)[q] = a;
+    } else {
+        constexpr int G = kWave / KG;
+        const int grp = lane / KG;
+        for (int l = lane % KG; l - lane % KG < k; l += KG) {  // one pass unless k > 64
+            const bool lok = l < k;
+            const int lc = lok ? l : k - 1;
+            float a = 0.f;
+            for (int64_t base = tb; base < te; base += (int64_t)G * U) {
+                float v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t t = base + u * G + grp;
+                    const int e = eid[t < te ? t : tb];
+                    v[u] = T[(size_t)(uint32_t)e * k + lc];
+                    if (t >= te) v[u] = 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) a += v[u];
+            }
+            for (int off = KG; off < kWave; off <<= 1) a += __shfl_xor(a, off);
+            if (grp == 0 && lok) dst[l] = a;
+        }
+    }
+}
+
+template <bool VEC, int KG>
+__global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restrict__ col_ptr,
+                                                         const int32_t *__restrict__ eid,
+                                                         const float *__restrict__ T,
+                                                         float *__restrict__ grad_cbsr,
+                                                         float *__restrict__ slab,
+                                                         int32_t *__restrict__ slab_row,
+                                                         int num_cols, int64_t num_e, int k,
+                                                         int chunk, int n_items) {
+    const int wid = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int item = blockIdx.x * kWavesPerBlock + wid;
+    if (item >= n_items) return;
+    const int64_t total = (int64_t)num_cols + num_e;
+    const int64_t d0 = (int64_t)item * chunk;
+    const int64_t d1 = d0 + chunk < total ? d0 + chunk : total;
+    int c = wave_first_row_token(col_ptr, num_cols, d0);
+    int cont = -1;
+    if (c > 0) {
+        const int64_t sb = d0 - c;
+        int64_t se = (int64_t)col_ptr[c];
+        if (d1 - c < se) se = d1 - c;
+        if (sb < se) {
+            segment_sum<VEC, KG>(T, eid, sb, se, k, slab + (int64_t)item * k, lane);
+            cont = c - 1;
+        }
+    }
+    if (lane == 0) slab_row[item] = cont;
+    for (; c < num_cols; ++c) {
+        const int64_t cb = col_ptr[c];
+        if (cb + c >= d1) break;
+        int64_t se = (int64_t)col_ptr[c + 1];
+        if (d1 - c - 1 < se) se = d1 - c - 1;
+        segment_sum<VEC, KG>(T, eid, cb, se, k, grad_cbsr + (int64_t)c * k, lane);
+    }
+}
+
+// grad_cbsr[row] += slabs of the split destination rows, in item order.
+__global__ __launch_bounds__(kBlock) void csc_sum_fixup_kernel(const float *__restrict__ slab,
+                                                               const int32_t *__restrict__ slab_row,
+                                                               float *__restrict__ out, int k,
+                                                               int n_items) {
+    const int wid = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int item = blockIdx.x * kWavesPerBlock + wid;
+    if (item >= n_items) return;
+    const int row = slab_row[item];
+    if (row < 0) return;
+    if (item > 0 && slab_row[item - 1] == row) return;
+    for (int j = lane; j < k; j += kWave) {
+        float a = out[(int64_t)row * k + j];
+        for (int i = item; i < n_items && slab_row[i] == row; ++i) a += slab[(int64_t)i * k + j];
+        out[(int64_t)row * k + j] = a;
+    }
 }
 
 int bwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk) {
@@ -129,6 +335,72 @@ int bwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk) {
     int64_t c = ceil_div(total, 256LL * 32 * 8);
     c = c < 256 ? 256 : (c > 2048 ? 2048 : c);
     return (int)c;
+}
+
+int n_items_for(int64_t rows, int64_t num_e, int chunk) {
+    const int64_t n = ceil_div(rows + num_e, chunk);
+    return (int)(n > 0 ? n : 1);
+}
+
+template <int MODE>
+int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
+                const float *edge_val, const float *grad, const float *row_div,
+                const uint8_t *cbsr_idx, float *dst, int nr, int64_t num_e, int D, int k,
+                int chunk) {
+    const int n_items = n_items_for(nr, num_e, chunk);
+    const dim3 grid((unsigned)ceil_div(n_items, kWavesPerBlock));
+    switch (lanes_per_edge(k)) {
+#define MAXK_CASE(KGV)                                                                        \
+    case KGV:                                                                                 \
+        hipLaunchKernelGGL((sspmm_bwd_kernel<KGV, (KGV >= 8 ? MAXK_BWD_U : 4), MODE>), grid,  \
+                           dim3(kBlock), 0, s, row_ptr, col_idx, edge_val, grad, row_div,     \
+                           cbsr_idx, dst, nr, num_e, D, k, chunk, n_items);                   \
+        break;
+        MAXK_CASE(1)
+        MAXK_CASE(2)
+        MAXK_CASE(4)
+        MAXK_CASE(8)
+        MAXK_CASE(16)
+        MAXK_CASE(32)
+        MAXK_CASE(64)
+#undef MAXK_CASE
+        default:
+            set_error("unsupported lane group");
+            return MAXK_ERR_INVALID;
+    }
+    MAXK_LAUNCHED("sspmm_bwd_kernel");
+    return MAXK_OK;
+}
+
+bool vec_sum(int k) { return k >= 4 && (k & (k - 1)) == 0; }
+
+struct CscLayout {
+    int chunk, n_items;
+    size_t t_bytes, slab_off, row_off, total;
+};
+
+CscLayout csc_layout(int64_t num_cols, int64_t num_e, int k, int chunk) {
+    CscLayout L{};
+    L.chunk = bwd_chunk(num_cols, num_e, chunk);
+    L.n_items = n_items_for(num_cols, num_e, L.chunk);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    L.t_bytes = al((size_t)(num_e + 1) * k * sizeof(float));  // + dummy row for masked lanes
+    L.slab_off = L.t_bytes;
+    L.row_off = L.slab_off + al((size_t)L.n_items * k * sizeof(float));
+    L.total = L.row_off + al((size_t)L.n_items * sizeof(int32_t));
+    return L;
+}
+
+int check_common(int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t D, int32_t k,
+                 int32_t chunk) {
+    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
+    MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
+    MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
+    MAXK_REQUIRE(D >= 1 && D <= kMaxDim, "dim_origin must be in [1,256], got %d", D);
+    MAXK_REQUIRE(k >= 1 && k <= D, "dim_k must be in [1,dim_origin], got %d", k);
+    MAXK_REQUIRE(chunk >= 0, "chunk_edges must be >= 0");
+    MAXK_REQUIRE(num_cols * (int64_t)k < (1LL << 31), "num_cols*k too large");
+    return MAXK_OK;
 }
 
 }  // namespace
@@ -153,15 +425,7 @@ extern "C" int maxk_sspmm_backward(const int32_t *row_ptr, const int32_t *col_id
                                    void *stream) {
     (void)workspace; (void)workspace_bytes;
     clear_error();
-    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
-    MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
-    MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
-    MAXK_REQUIRE(dim_origin >= 1 && dim_origin <= kMaxDim, "dim_origin must be in [1,256], got %d",
-                 dim_origin);
-    MAXK_REQUIRE(dim_k >= 1 && dim_k <= dim_origin, "dim_k must be in [1,dim_origin], got %d",
-                 dim_k);
-    MAXK_REQUIRE(chunk_edges >= 0, "chunk_edges must be >= 0");
-    MAXK_REQUIRE(num_cols * (int64_t)dim_k < (1LL << 31), "num_cols*k too large");
+    if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges)) return rc;
     hipStream_t s = as_stream(stream);
     if (num_cols > 0) {
         MAXK_REQUIRE(grad_cbsr != nullptr, "grad_cbsr must not be NULL");
@@ -171,30 +435,78 @@ extern "C" int maxk_sspmm_backward(const int32_t *row_ptr, const int32_t *col_id
     MAXK_REQUIRE(row_ptr && col_idx && edge_val && grad_out && cbsr_idx,
                  "CSR/grad/selector pointers must not be NULL");
     MAXK_REQUIRE(num_cols > 0, "edges present but num_cols == 0");
+    return launch_push<kAtomic>(s, row_ptr, col_idx, edge_val, grad_out, row_div, cbsr_idx,
+                                grad_cbsr, (int)num_rows, num_e, dim_origin, dim_k,
+                                bwd_chunk(num_rows, num_e, chunk_edges));
+}
 
-    const int chunk = bwd_chunk(num_rows, num_e, chunk_edges);
-    const int64_t n64 = ceil_div(num_rows + num_e, chunk);
-    const int n_items = (int)(n64 > 0 ? n64 : 1);
-    const dim3 grid((unsigned)ceil_div(n_items, kWavesPerBlock));
-    const int nr = (int)num_rows, D = dim_origin, k = dim_k;
-    switch (lanes_per_edge(dim_k)) {
-#define MAXK_CASE(KGV)                                                                      \
-    case KGV:                                                                               \
-        launch_bwd<KGV>(grid, s, row_ptr, col_idx, edge_val, grad_out, row_div, cbsr_idx,   \
-                        grad_cbsr, nr, num_e, D, k, chunk, n_items);                        \
-        break;
-        MAXK_CASE(1)
-        MAXK_CASE(2)
-        MAXK_CASE(4)
-        MAXK_CASE(8)
-        MAXK_CASE(16)
-        MAXK_CASE(32)
-        MAXK_CASE(64)
-#undef MAXK_CASE
-        default:
-            set_error("unsupported lane group");
-            return MAXK_ERR_INVALID;
+extern "C" size_t maxk_sspmm_backward_csc_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                         int64_t num_e, int32_t dim_origin,
+                                                         int32_t dim_k, int32_t chunk_edges) {
+    (void)num_rows; (void)dim_origin;
+    if (num_cols < 0 || num_e < 0 || dim_k <= 0) return 0;
+    return csc_layout(num_cols, num_e, dim_k, chunk_edges).total;
+}
+
+extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *col_idx,
+                                       const float *edge_val, const float *grad_out,
+                                       const float *row_div, const uint8_t *cbsr_idx,
+                                       const int32_t *col_ptr, const int32_t *csc_eid,
+                                       float *grad_cbsr, int64_t num_rows, int64_t num_cols,
+                                       int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                                       int32_t chunk_edges, void *workspace,
+                                       size_t workspace_bytes, void *stream) {
+    clear_error();
+    if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges)) return rc;
+    hipStream_t s = as_stream(stream);
+    if (num_cols == 0) return MAXK_OK;
+    MAXK_REQUIRE(grad_cbsr && col_ptr, "grad_cbsr/col_ptr must not be NULL");
+    MAXK_REQUIRE(num_e == 0 || (row_ptr && col_idx && edge_val && grad_out && cbsr_idx &&
+                                csc_eid),
+                 "CSR/grad/selector/transpose pointers must not be NULL");
+    const CscLayout L = csc_layout(num_cols, num_e, dim_k, chunk_edges);
+    MAXK_REQUIRE(workspace && workspace_bytes >= L.total,
+                 "workspace too small: need %zu bytes, got %zu", L.total, workspace_bytes);
+    char *ws = reinterpret_cast<char *>(workspace);
+    float *T = reinterpret_cast<float *>(ws);
+    float *slab = reinterpret_cast<float *>(ws + L.slab_off);
+    int32_t *slab_row = reinterpret_cast<int32_t *>(ws + L.row_off);
+    const int k = dim_k;
+    if (num_e > 0 && num_rows > 0) {
+        if (int rc = launch_push<kStore>(s, row_ptr, col_idx, edge_val, grad_out, row_div,
+                                         cbsr_idx, T, (int)num_rows, num_e, dim_origin,
+                                         k, bwd_chunk(num_rows, num_e, chunk_edges)))
+            return rc;
     }
-    MAXK_LAUNCHED("sspmm_bwd_kernel");
+    const dim3 grid((unsigned)ceil_div(L.n_items, kWavesPerBlock));
+    const int nc = (int)num_cols;
+    if (vec_sum(k)) {
+        hipLaunchKernelGGL((csc_sum_kernel<true, 64>), grid, dim3(kBlock), 0, s, col_ptr, csc_eid, T,
+                           grad_cbsr, slab, slab_row, nc, num_e, k, L.chunk, L.n_items);
+    } else {
+        switch (lanes_per_edge(k)) {
+#define MAXK_CASE(KGV)                                                                        \
+    case KGV:                                                                                 \
+        hipLaunchKernelGGL((csc_sum_kernel<false, KGV>), grid, dim3(kBlock), 0, s, col_ptr,    \
+                           csc_eid, T,                                                        \
+                           grad_cbsr, slab, slab_row, nc, num_e, k, L.chunk, L.n_items);      \
+        break;
+            MAXK_CASE(1)
+            MAXK_CASE(2)
+            MAXK_CASE(4)
+            MAXK_CASE(8)
+            MAXK_CASE(16)
+            MAXK_CASE(32)
+            MAXK_CASE(64)
+#undef MAXK_CASE
+            default:
+                set_error("unsupported lane group");
+                return MAXK_ERR_INVALID;
+        }
+    }
+    MAXK_LAUNCHED("csc_sum_kernel");
+    hipLaunchKernelGGL(csc_sum_fixup_kernel, grid, dim3(kBlock), 0, s, slab, slab_row, grad_cbsr,
+                       k, L.n_items);
+    MAXK_LAUNCHED("csc_sum_fixup_kernel");
     return MAXK_OK;
 }

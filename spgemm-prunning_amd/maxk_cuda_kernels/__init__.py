@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import List, Optional, Tuple
 
 import torch
@@ -38,6 +39,7 @@ __all__ = [
     # MI355X additions
     "topk_cbsr", "cbsr_scatter_dense", "build_warp4_metadata", "warp4_to_indptr",
     "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
+    "transpose_plan",
 ]
 
 FULL_DIM = 256  # the reference binding's fixed output width (cuda_kernel_bindings.cpp:70)
@@ -184,7 +186,7 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             raise RuntimeError("out must be [num_rows, dim_origin]")
     L = _lib()
     E = indices.numel()
-    ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, E, D, k, chunk)
+    ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, num_cols, E, D, k, chunk)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
         _capi.check(L.maxk_spgemm_forward(
@@ -194,12 +196,56 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     return out
 
 
+_PLAN_CACHE: "dict" = {}
+
+
+def transpose_plan(indices: torch.Tensor, num_cols: int, cache: bool = True):
+    """(col_ptr int32 [num_cols+1], csc_eid int32 [E]) of the CSR column indices: the CSC
+    pointer and, per CSC slot, the CSR edge id it holds.  Built once per graph on the GPU
+    (stable radix sort); cached per `indices` tensor object (and its version counter)."""
+    _need(indices, "indices", torch.int32)
+    key = id(indices)
+    hit = _PLAN_CACHE.get(key)
+    if cache and hit is not None:
+        ref, nc, ver, plan = hit
+        if ref() is indices and nc == num_cols and ver == indices._version:
+            return plan
+    dev = indices.device
+    E = indices.numel()
+    col_ptr = torch.empty(num_cols + 1, dtype=torch.int32, device=dev)
+    csc_eid = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
+    L = _lib()
+    ws = torch.empty(max(1, L.maxk_transpose_plan_workspace_size(num_cols, E)), dtype=torch.uint8,
+                     device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(L.maxk_transpose_plan(_ptr(indices), num_cols, E, _ptr(col_ptr),
+                                          _ptr(csc_eid), _ptr(ws), ws.numel(), _stream(dev)),
+                    "maxk_transpose_plan")
+    plan = (col_ptr, csc_eid)
+    if cache:
+        if key not in _PLAN_CACHE:
+            weakref.finalize(indices, _PLAN_CACHE.pop, key, None)
+        _PLAN_CACHE[key] = (weakref.ref(indices), int(num_cols), indices._version, plan)
+    return plan
+
+
+def _bwd_mode(mode: Optional[str]) -> str:
+    mode = mode or os.environ.get("MAXK_BWD_MODE", "csc")
+    if mode not in ("csc", "atomic"):
+        raise RuntimeError(f"backward mode must be 'csc' or 'atomic', got {mode!r}")
+    return mode
+
+
 def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
                    grad_output: torch.Tensor, cbsr_idx: torch.Tensor,
                    row_div: Optional[torch.Tensor] = None, chunk: int = 0,
-                   out: Optional[torch.Tensor] = None, validate: Optional[bool] = None
-                   ) -> torch.Tensor:
-    """grad_cbsr[num_cols, k] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]]."""
+                   out: Optional[torch.Tensor] = None, validate: Optional[bool] = None,
+                   mode: Optional[str] = None, plan=None) -> torch.Tensor:
+    """grad_cbsr[num_cols, k] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]].
+
+    mode "csc" (default; MAXK_BWD_MODE overrides): two-phase, atomic-free and bitwise
+    deterministic, using the graph's transpose plan (built once and cached, or `plan=`).
+    mode "atomic": one global fp32 atomic per (edge, l); no preprocessing."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32), (grad_output, "grad_output", torch.float32),
                      (cbsr_idx, "sparse_selector", torch.uint8)):
@@ -225,13 +271,23 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             raise RuntimeError("out must be [num_cols, k]")
     L = _lib()
     E = indices.numel()
-    ws_bytes = L.maxk_sspmm_backward_workspace_size(num_rows, num_cols, E, D, k, chunk)
+    if _bwd_mode(mode) == "atomic":
+        ws_bytes = L.maxk_sspmm_backward_workspace_size(num_rows, num_cols, E, D, k, chunk)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            _capi.check(L.maxk_sspmm_backward(
+                _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
+                _ptr(cbsr_idx), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws),
+                ws.numel(), _stream(dev)), "maxk_sspmm_backward")
+        return out
+    col_ptr, csc_eid = plan if plan is not None else transpose_plan(indices, num_cols)
+    ws_bytes = L.maxk_sspmm_backward_csc_workspace_size(num_rows, num_cols, E, D, k, chunk)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
-        _capi.check(L.maxk_sspmm_backward(
+        _capi.check(L.maxk_sspmm_backward_csc(
             _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
-            _ptr(cbsr_idx), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws), ws.numel(),
-            _stream(dev)), "maxk_sspmm_backward")
+            _ptr(cbsr_idx), _ptr(col_ptr), _ptr(csc_eid), _ptr(out), num_rows, num_cols, E, D,
+            k, chunk, _ptr(ws), ws.numel(), _stream(dev)), "maxk_sspmm_backward_csc")
     return out
 
 

@@ -28,12 +28,17 @@ SIGNATURES = {
     "maxk_version": (ctypes.c_int, []),
     "maxk_last_error": (ctypes.c_char_p, []),
     "maxk_device_count": (ctypes.c_int, []),
-    "maxk_spgemm_forward_workspace_size": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "maxk_spgemm_forward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_spgemm_forward": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),
     "maxk_sspmm_backward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),
+    "maxk_sspmm_backward_csc_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
+    "maxk_sspmm_backward_csc": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64,
+                                               _i64, _i32, _i32, _i32, _p, _sz, _p]),
+    "maxk_transpose_plan_workspace_size": (_sz, [_i64, _i64]),
+    "maxk_transpose_plan": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _sz, _p]),
     "maxk_topk_cbsr": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_u8": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_cbsr_scatter_dense": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),

@@ -70,10 +70,10 @@ def test_workspace_sizes():
     from maxk_cuda_kernels import _capi
     L = _capi.load()
     # slabs: one D-row per work item + a row id per item
-    n = L.maxk_spgemm_forward_workspace_size(1000, 100000, 256, 16, 512)
+    n = L.maxk_spgemm_forward_workspace_size(1000, 1000, 100000, 256, 16, 512)
     items = -(-101000 // 512)
-    assert n >= items * (256 * 4 + 4)
-    assert L.maxk_spgemm_forward_workspace_size(0, 0, 256, 16, 0) > 0  # one item minimum
+    assert n >= items * (256 * 4 + 4) + 1000 * 128  # slabs + row ids + packed CBSR records
+    assert L.maxk_spgemm_forward_workspace_size(0, 0, 0, 256, 16, 0) > 0  # one item minimum
     assert L.maxk_warp4_build_workspace_size(1000) >= 2 * 4000
 
 

@@ -65,14 +65,34 @@ def test_forward_golden(mk, cuda, path, chunk):
     close(y, z["y_ref"])
 
 
+@pytest.mark.parametrize("mode", ["csc", "atomic"])
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
-def test_backward_golden(mk, cuda, path, chunk):
+def test_backward_golden(mk, cuda, path, chunk, mode):
     z = load_golden(path)
     gs = mk.sspmm_backward(T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda),
                            T(z["g"], cuda), T(z["topk_idx"], cuda), row_div=T(z["deg"], cuda),
-                           chunk=chunk)
+                           chunk=chunk, mode=mode)
     close(gs, z["grad_cbsr_ref"])
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_transpose_plan(mk, cuda, path):
+    z = load_golden(path)
+    V = z["row_ptr"].size - 1
+    col_ptr, eid = mk.transpose_plan(T(z["col_idx"], cuda), V)
+    tp, _, _ = O.transpose_csr(z["row_ptr"], z["col_idx"], z["val"])
+    assert np.array_equal(col_ptr.cpu().numpy(), tp)
+    order = np.argsort(z["col_idx"], kind="stable")  # CSC slot t holds CSR edge order[t]
+    assert np.array_equal(eid.cpu().numpy(), order)
+
+
+def test_csc_backward_is_deterministic(mk, cuda):
+    z = load_golden(CASES[2])
+    args = [T(z[n], cuda) for n in ("row_ptr", "col_idx", "val", "g", "topk_idx")]
+    a = mk.sspmm_backward(*args, row_div=T(z["deg"], cuda), chunk=11, mode="csc")
+    b = mk.sspmm_backward(*args, row_div=T(z["deg"], cuda), chunk=11, mode="csc")
+    assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("path", CASES, ids=IDS)
@@ -151,11 +171,11 @@ def rand_graph(rng, V, avg, hubs=(), empty=0, cols=None):
     return row_ptr.astype(np.int32), col.astype(np.int32)
 
 
-def run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div=None, chunk=0):
+def run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div=None, chunk=0, mode=None):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
                           D, row_div=None if div is None else T(div, cuda), chunk=chunk)
     gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda),
-                           row_div=None if div is None else T(div, cuda), chunk=chunk)
+                           row_div=None if div is None else T(div, cuda), chunk=chunk, mode=mode)
     yo = O.spgemm_fwd(row_ptr, col, val, cv, ci, D, row_div=div)
     go = O.sspmm_bwd(row_ptr, col, val, g, ci, row_div=div)
     return y, yo, gs, go
@@ -173,8 +193,8 @@ def test_all_k_against_oracle(mk, cuda, k, D):
     cv, ci = O.topk(x, k)
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-    for chunk in (0, 13):
-        y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, chunk)
+    for chunk, mode in ((0, "csc"), (13, "csc"), (13, "atomic")):
+        y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, chunk, mode)
         close(y, yo)
         close(gs, go)
     v, i = mk.topk_cbsr(T(x, cuda), k)
@@ -198,9 +218,11 @@ def test_empty_graph_and_empty_rows(mk, cuda):
     col = np.array([0, 5, 49], np.int32)
     val = np.array([1.0, 2.0, 3.0], np.float32)
     for chunk in (0, 1, 2, 7):
-        y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=chunk)
-        close(y, yo)
-        close(gs, go)
+        for mode in ("csc", "atomic"):
+            y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=chunk,
+                                     mode=mode)
+            close(y, yo)
+            close(gs, go)
 
 
 def test_output_fully_overwritten(mk, cuda):
@@ -215,10 +237,11 @@ def test_output_fully_overwritten(mk, cuda):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
                           D, out=out, chunk=9)
     close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, D))
-    gout = torch.full((V, k), float("nan"), device=cuda)
-    gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda),
-                           out=gout)
-    close(gs, O.sspmm_bwd(row_ptr, col, val, g, ci))
+    for mode in ("csc", "atomic"):
+        gout = torch.full((V, k), float("nan"), device=cuda)
+        gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
+                               T(ci, cuda), out=gout, mode=mode, chunk=7)
+        close(gs, O.sspmm_bwd(row_ptr, col, val, g, ci))
 
 
 def test_duplicate_selectors_accumulate(mk, cuda):
@@ -244,10 +267,11 @@ def test_rectangular_shard(mk, cuda):
     val = rng.random(col.size, dtype=np.float32)
     cv, ci = O.topk(rng.standard_normal((C, D), dtype=np.float32), k)
     g = rng.standard_normal((R, D), dtype=np.float32)
-    y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=64)
-    assert y.shape == (R, D) and gs.shape == (C, k)
-    close(y, yo)
-    close(gs, go)
+    for mode in ("csc", "atomic"):
+        y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=64, mode=mode)
+        assert y.shape == (R, D) and gs.shape == (C, k)
+        close(y, yo)
+        close(gs, go)
 
 
 def test_topk_ties_nan_and_uint8(mk, cuda):
@@ -334,6 +358,8 @@ def test_adjoint_identity_large(mk, cuda):
     a = (y.double() * G.double()).sum().item()
     b = (v.double() * gs.double()).sum().item()
     assert abs(a - b) <= 1e-4 * max(1.0, abs(a))
+    gs_atomic = mk.sspmm_backward(row_ptr, dst, val, G, sel, mode="atomic")
+    assert torch.allclose(gs, gs_atomic, rtol=1e-4, atol=1e-4)
     # row sums: sum_j Y[r, j] == A . (sum_l v[c, l])
     rs = torch.sparse_csr_tensor(row_ptr.long(), dst.long(), val, (V, V)) @ v.sum(1, keepdim=True)
     assert torch.allclose(y.sum(1), rs[:, 0], rtol=1e-4, atol=1e-3)
