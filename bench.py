@@ -44,6 +44,28 @@ PRESETS = {
 }
 
 
+# kernels making up each op of one step (rocprofv3 names, maxk:: namespace)
+OP_KERNELS = {
+    "spgemm_forward": ["cbsr_pack_kernel", "spgemm_fwd_kernel", "spgemm_fwd_fixup_kernel"],
+    "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "csc_sum_fixup_kernel"],
+    "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
+}
+
+
+def load_traffic(key, op):
+    """Per-launch HBM bytes of `op` on workload `key` from the newest profiles/rNN/traffic.json
+    (written by tools/pmc_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes of this same bench command; FETCH_SIZE doubled per MI355X_MICROARCH.md, HBM)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")),
+                       reverse=True):
+        with open(path) as f:
+            t = json.load(f)
+        if key in t and op in t[key]:
+            return t[key][op]["bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -180,21 +202,14 @@ def main():
         log(f"[bench] graph {args.graph}: V={V} E={E} max_deg={int(deg.max())} "
             f"avg_deg={E / V:.1f} gen {time.time() - t0:.1f}s")
 
-    # ---- shard by vertex range, balanced by nnz
+    # ---- shard by vertex range, balanced by nnz (maxk_dist: the module the gloo tests cover)
     if world > 1:
-        bounds = torch.searchsorted(row_ptr.long(), torch.arange(world + 1, device=dev) * E // world)
-        bounds[0], bounds[-1] = 0, V
-        bnd = bounds.tolist()
-        v0, v1 = bnd[rank], bnd[rank + 1]
-        vmax = max(bnd[i + 1] - bnd[i] for i in range(world))
-        e0, e1 = int(row_ptr[v0]), int(row_ptr[v1])
-        l_row_ptr = (row_ptr[v0:v1 + 1] - e0).contiguous()
-        owner = torch.searchsorted(torch.tensor(bnd[1:], device=dev), col.long()[e0:e1], right=True)
-        l_col = (owner * vmax + (col.long()[e0:e1] - torch.tensor(bnd, device=dev)[owner])).int()
-        l_val = val[e0:e1].contiguous()
+        import maxk_dist
+        shard = maxk_dist.ShardedMaxK(row_ptr, col, val, rank, world, device=dev)
+        v0, v1, vmax, n_cols = shard.v0, shard.v1, shard.vmax, shard.n_cols
+        l_row_ptr, l_col, l_val = shard.row_ptr, shard.col_idx, shard.values
         l_X = X[v0:v1]
         l_G = G[v0:v1].contiguous()
-        n_cols = world * vmax
     else:
         v0, v1, vmax = 0, V, V
         l_row_ptr, l_col, l_val, l_X, l_G, n_cols = row_ptr, col, val, X, G, V
@@ -281,9 +296,12 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = 2.0 * E * args.steps / elapsed / 1e9
     B_f, B_b = alg_bytes(nl, El, D, k, n_cols)
-    kern = "sspmm_bwd_kernel" if bwd_avg >= fwd_avg else "spgemm_fwd_kernel"
-    t_dom, B_dom = (bwd_avg, B_b) if bwd_avg >= fwd_avg else (fwd_avg, B_f)
+    bwd_op = f"sspmm_backward_{args.bwd_mode}"
+    op, t_dom, B_dom = (bwd_op, bwd_avg, B_b) if bwd_avg >= fwd_avg else \
+        ("spgemm_forward", fwd_avg, B_f)
     achieved = B_dom / (t_dom * 1e-3) / 1e9
+    tkey = f"{args.graph}-D{D}-k{k}-{args.bwd_mode}-n{world}"
+    traffic, traffic_src = load_traffic(tkey, op)
 
     extra = {
         "fwd_ms": round(fwd_avg, 4), "bwd_ms": round(bwd_avg, 4),
@@ -341,11 +359,12 @@ def main():
                 "graph": args.graph, "V": V, "E": E, "D": D, "k": k,
                 "parallelism": f"vertex-range x{world}" if world > 1 else "single-gpu",
             },
-            "roofline": {"bound": "hbm", "kernel": kern, "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "alg_bytes_per_launch": B_dom,
-                         "launch_ms": round(t_dom, 4)},
+                         "traffic": traffic, "op": op, "kernels": OP_KERNELS[op],
+                         "alg_bytes_per_launch": B_dom, "launch_ms": round(t_dom, 4),
+                         "traffic_source": traffic_src, "traffic_key": tkey},
             "cpu_baseline": cpu,
             "extra": extra,
         }

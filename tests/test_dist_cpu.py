@@ -1,0 +1,194 @@
+"""Multi-process (gloo, CPU) tests of the sharded aggregation.
+
+The HIP kernels are replaced by the oracle (test infrastructure) through the
+`kernels=` hook, so what is checked here is the distributed logic itself:
+nnz-balanced partition, column remap to the padded space, all-gather of the
+CBSR rows, reduce-scatter of the gradient partials, autograd plumbing.  Each
+rank's slice must equal the 1-process oracle result (forward bit-exact: every
+output row is computed whole on its owner; backward within 1e-5 relative,
+since the reduce-scatter sums per-rank partials in a different order).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import conftest  # noqa: F401  (sys.path: package, oracle)
+import maxk_dist
+import oracle
+
+BWD_ATOL = 1e-5
+
+
+class OracleKernels:
+    """kernels= backend for ShardedMaxK built on the CPU oracle (tests only)."""
+
+    def spgemm_forward(self, indptr, indices, values, cbsr_val, cbsr_idx, D, row_div=None):
+        y = oracle.spgemm_fwd(indptr.numpy(), indices.numpy(), values.numpy(), cbsr_val.numpy(),
+                              cbsr_idx.numpy(), D,
+                              row_div=None if row_div is None else row_div.numpy())
+        return torch.from_numpy(y)
+
+    def sspmm_backward(self, indptr, indices, values, grad, cbsr_idx, row_div=None, plan=None):
+        g = oracle.sspmm_bwd(indptr.numpy(), indices.numpy(), values.numpy(), grad.numpy(),
+                             cbsr_idx.numpy(),
+                             row_div=None if row_div is None else row_div.numpy())
+        return torch.from_numpy(g)
+
+
+def make_graph(V, avg_deg, seed, hub=True):
+    rng = np.random.default_rng(seed)
+    deg = rng.poisson(avg_deg, V).astype(np.int64)
+    if hub:
+        deg[V // 3] = 8 * avg_deg * 10  # one heavy row makes the nnz split uneven in rows
+    if V > 5:
+        deg[5] = 0  # an empty row
+    row_ptr = np.zeros(V + 1, dtype=np.int64)
+    np.cumsum(deg, out=row_ptr[1:])
+    E = int(row_ptr[-1])
+    col = rng.integers(0, V, E).astype(np.int32)
+    val = rng.standard_normal(E).astype(np.float32)
+    return row_ptr.astype(np.int32), col, val
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, V, D, k, seed, use_div, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        row_ptr, col, val = make_graph(V, 6, seed)
+        rng = np.random.default_rng(seed + 1)
+        x = rng.standard_normal((V, D)).astype(np.float32)
+        tv, ti = oracle.topk(x, k)
+        g = rng.standard_normal((V, D)).astype(np.float32)
+        deg = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+
+        shard = maxk_dist.ShardedMaxK(torch.from_numpy(row_ptr), torch.from_numpy(col),
+                                      torch.from_numpy(val), rank, world,
+                                      kernels=OracleKernels())
+        v0, v1 = shard.v0, shard.v1
+        div = torch.from_numpy(deg[v0:v1]) if use_div else None
+        val_l = torch.from_numpy(tv[v0:v1]).requires_grad_(True)
+        y = maxk_dist.sharded_maxk_spgemm(shard, val_l, torch.from_numpy(ti[v0:v1]), D, div)
+        y.backward(torch.from_numpy(g[v0:v1]))
+        q.put((rank, v0, v1, y.detach().numpy(), val_l.grad.numpy(), shard.bounds))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # surface the failure to the parent
+        q.put((rank, "error", repr(e)))
+        raise
+
+
+def _run(world, V=400, D=64, k=8, seed=0, use_div=True):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, V, D, k, seed, use_div, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for o in outs:
+        assert o[1] != "error", o
+    return sorted(outs)
+
+
+def _single(V, D, k, seed, use_div):
+    row_ptr, col, val = make_graph(V, 6, seed)
+    rng = np.random.default_rng(seed + 1)
+    x = rng.standard_normal((V, D)).astype(np.float32)
+    tv, ti = oracle.topk(x, k)
+    g = rng.standard_normal((V, D)).astype(np.float32)
+    deg = np.maximum(np.diff(row_ptr), 1).astype(np.float32) if use_div else None
+    y = oracle.spgemm_fwd(row_ptr, col, val, tv, ti, D, row_div=deg)
+    gs = oracle.sspmm_bwd(row_ptr, col, val, g, ti, row_div=deg)
+    return y, gs
+
+
+@pytest.mark.parametrize("world,use_div", [(2, True), (3, False)])
+def test_sharded_matches_single_process(world, use_div):
+    V, D, k, seed = 400, 64, 8, 7
+    outs = _run(world, V, D, k, seed, use_div)
+    y_ref, gs_ref = _single(V, D, k, seed, use_div)
+    covered = 0
+    for rank, v0, v1, y, gs, bounds in outs:
+        assert bounds[0] == 0 and bounds[-1] == V
+        np.testing.assert_array_equal(y, y_ref[v0:v1])
+        np.testing.assert_allclose(gs, gs_ref[v0:v1], rtol=1e-5, atol=BWD_ATOL)
+        covered += v1 - v0
+    assert covered == V
+
+
+def test_balanced_bounds_properties():
+    row_ptr, _, _ = make_graph(1000, 5, 3)
+    rp = torch.from_numpy(row_ptr)
+    for world in (1, 2, 3, 8, 16):
+        b = maxk_dist.balanced_bounds(rp, world)
+        assert len(b) == world + 1 and b[0] == 0 and b[-1] == 1000
+        assert all(b[i] <= b[i + 1] for i in range(world))
+        E = int(row_ptr[-1])
+        max_row = int(np.diff(row_ptr).max())
+        for i in range(world):
+            nnz = int(row_ptr[b[i + 1]] - row_ptr[b[i]])
+            assert nnz <= E // world + max_row + 1
+    # more shards than rows: some shards are empty, still a valid partition
+    b = maxk_dist.balanced_bounds(torch.tensor([0, 3, 3, 5], dtype=torch.int32), 5)
+    assert b[0] == 0 and b[-1] == 3 and all(b[i] <= b[i + 1] for i in range(5))
+
+
+def test_column_remap_single_rank():
+    """world=1 is the identity remap; the remapped column of a vertex is owner*vmax+offset."""
+    row_ptr, col, val = make_graph(200, 4, 11, hub=False)
+    rp, ci, va = map(torch.from_numpy, (row_ptr, col, val))
+    s = maxk_dist.ShardedMaxK(rp, ci, va, 0, 1, kernels=OracleKernels())
+    assert torch.equal(s.col_idx, ci) and torch.equal(s.row_ptr, rp)
+    b = [0, 50, 120, 200]
+    s1 = maxk_dist.ShardedMaxK(rp, ci, va, 1, 3, kernels=OracleKernels(), bounds=b)
+    assert s1.vmax == 80 and s1.n_cols == 240 and (s1.v0, s1.v1) == (50, 120)
+    e0, e1 = int(row_ptr[50]), int(row_ptr[120])
+    cols = col[e0:e1].astype(np.int64)
+    owner = np.searchsorted(np.array(b[1:]), cols, side="right")
+    np.testing.assert_array_equal(s1.col_idx.numpy(), owner * 80 + cols - np.array(b)[owner])
+
+
+@pytest.mark.gpu
+def test_sharded_hip_single_rank_rccl(cuda):
+    """ShardedMaxK over RCCL (world 1) with the HIP kernels == the direct HIP calls == oracle."""
+    import maxk_cuda_kernels as mk
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
+    try:
+        V, D, k = 3000, 256, 16
+        row_ptr, col, val = make_graph(V, 9, 5)
+        rng = np.random.default_rng(2)
+        x = rng.standard_normal((V, D)).astype(np.float32)
+        g = rng.standard_normal((V, D)).astype(np.float32)
+        deg = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+        tv, ti = oracle.topk(x, k)
+        to = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
+        shard = maxk_dist.ShardedMaxK(to(row_ptr), to(col), to(val), 0, 1, device=cuda)
+        val_l = to(tv).requires_grad_(True)
+        y = maxk_dist.sharded_maxk_spgemm(shard, val_l, to(ti), D, to(deg))
+        y.backward(to(g))
+        y_ref = oracle.spgemm_fwd(row_ptr, col, val, tv, ti, D, row_div=deg)
+        gs_ref = oracle.sspmm_bwd(row_ptr, col, val, g, ti, row_div=deg)
+        np.testing.assert_allclose(y.detach().cpu().numpy(), y_ref, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(val_l.grad.cpu().numpy(), gs_ref, rtol=1e-4, atol=1e-4)
+        y2 = mk.spgemm_forward(to(row_ptr), to(col), to(val), to(tv), to(ti), D, row_div=to(deg))
+        assert torch.equal(y.detach(), y2)
+    finally:
+        dist.destroy_process_group()

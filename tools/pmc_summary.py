@@ -1,10 +1,23 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc counter CSVs per kernel (mean per dispatch).
+
 FETCH_SIZE/WRITE_SIZE are KB; on gfx950 FETCH_SIZE reads 1/2 of wide streaming
-bytes (MI355X_MICROARCH.md, HBM) -- the corrected column doubles it."""
+bytes (MI355X_MICROARCH.md, HBM) -- the corrected column doubles it.
+
+  pmc_summary.py CSV... [--traffic-out profiles/rNN/traffic.json --key WORKLOAD]
+
+With --traffic-out, per-op HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE summed over
+the op's kernels, bench.OP_KERNELS) are merged into that JSON under WORKLOAD (bench.py's
+traffic_key, e.g. reddit-D256-k16-csc-n1), where bench.py reads them as roofline.traffic.
+"""
+import argparse
 import collections
 import csv
+import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def short(n):
@@ -12,13 +25,23 @@ def short(n):
     return n.split("(")[0]
 
 
-def main(paths):
+def base(n):
+    return short(n).replace("maxk::", "").split("<")[0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv", nargs="+")
+    ap.add_argument("--traffic-out")
+    ap.add_argument("--key")
+    a = ap.parse_args()
     d = collections.defaultdict(list)
-    for p in paths:
+    for p in a.csv:
         for r in csv.DictReader(open(p)):
             if "maxk" not in r["Kernel_Name"]:
                 continue
             d[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+    per_kernel = collections.defaultdict(dict)  # base name -> counter -> mean bytes
     for (k, c), v in sorted(d.items()):
         m = sum(v) / len(v)
         extra = ""
@@ -26,8 +49,30 @@ def main(paths):
             extra = f"  -> {m * 1024 / 1e9:.3f} GB raw, {2 * m * 1024 / 1e9:.3f} GB x2-corrected"
         elif c == "WRITE_SIZE":
             extra = f"  -> {m * 1024 / 1e9:.3f} GB"
+        if c in ("FETCH_SIZE", "WRITE_SIZE"):
+            per_kernel[base(k)][c] = per_kernel[base(k)].get(c, 0.0) + m * 1024
         print(f"{k[:48]:48s} {c:14s} n={len(v):3d} mean={m:.5g}{extra}")
+    if a.traffic_out:
+        from bench import OP_KERNELS
+        out = {}
+        if os.path.exists(a.traffic_out):
+            out = json.load(open(a.traffic_out))
+        ops = {}
+        for op, ks in OP_KERNELS.items():
+            if not all(k in per_kernel for k in ks[:2]):
+                continue
+            if op.startswith("sspmm_backward_") and f"-{op.rsplit('_', 1)[1]}-" not in a.key:
+                continue  # the key names the backward mode the counters were taken in
+            f = sum(per_kernel.get(k, {}).get("FETCH_SIZE", 0.0) for k in ks)
+            w = sum(per_kernel.get(k, {}).get("WRITE_SIZE", 0.0) for k in ks)
+            ops[op] = {"bytes": int(2 * f + w), "fetch_raw": int(f), "write": int(w),
+                       "kernels": {k: per_kernel.get(k, {}) for k in ks}}
+        out[a.key] = ops
+        with open(a.traffic_out, "w") as fh:
+            json.dump(out, fh, indent=1, sort_keys=True)
+        print(f"wrote {a.traffic_out} [{a.key}]: " +
+              ", ".join(f"{op} {v['bytes'] / 1e9:.3f} GB" for op, v in ops.items()))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    main()
