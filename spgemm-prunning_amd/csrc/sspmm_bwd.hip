@@ -25,7 +25,95 @@
 namespace maxk {
 namespace {
 
-enum { kAtomic = 0, kStore = 1 };
+enum { kAtomic = 0, kStore = 1, kStoreX4 = 2 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// kStoreX4 (k % 4 == 0): LR = pow2ceil(k/4) lanes per edge, each lane owning 4
+// consecutive l: one u32 selector load, four LDS reads, one 16-B store; 64/LR
+// edges per wave step (4x fewer memory instructions per edge than one l per
+// lane).  T rows [sb, se) are addressed through a wave-uniform buffer
+// descriptor; a masked lane's offset lies past its end and the hardware drops
+// the store, so no store is predicated and no dummy row is touched.  Cache
+// policy of the T stores: MAXK_T_AUX (0 plain, 2 nt, 16 sc1).  Store lag as in
+// push_edges below.
+template <int LR, int U>
+__device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__restrict__ col_idx,
+                                        const float *__restrict__ edge_val,
+                                        const uint8_t *__restrict__ cbsr_idx,
+                                        float *__restrict__ T, int sb, int se, int k, int lane) {
+    constexpr int G = kWave / LR;
+    constexpr int GU = G * U;
+    constexpr uint32_t kDrop = 0x80000000u;
+    const int grp = lane / LR;
+    const int q = lane % LR;
+    const int k4 = k >> 2;
+    const bool qok = q < k4;
+    const int qc = qok ? q : k4 - 1;
+    const int last = se - 1;
+    const uint64_t tb = reinterpret_cast<uint64_t>(T + (size_t)(uint32_t)sb * k);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)tb);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane((se - sb) * k * 4);  // <= 2 MiB per segment
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, nbytes, 0x00020000);
+    const uint8_t *sel = cbsr_idx + 4 * qc;
+    int c[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = sb + u * G + grp;
+        const int ec = e < se ? e : last;
+        c[u] = ld_stream(col_idx + ec);
+        w[u] = ld_stream(edge_val + ec);
+    }
+    u32x4 xp[U];
+    uint32_t op[U];
+    bool pending = false;
+    for (int base = sb;; base += GU) {
+        const bool has_next = base + GU < se;  // wave-uniform
+        int cn[U];
+        float wn[U];
+        if (has_next) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = base + GU + u * G + grp;
+                const int ec = e < se ? e : last;
+                cn[u] = ld_stream(col_idx + ec);
+                wn[u] = ld_stream(edge_val + ec);
+            }
+        }
+        uint32_t sv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            sv[u] = *reinterpret_cast<const uint32_t *>(sel + (size_t)(uint32_t)c[u] * k);
+        if (pending) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                __builtin_amdgcn_raw_buffer_store_b128(xp[u], rsrc, (int)op[u], 0, MAXK_T_AUX);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = base + u * G + grp;
+            const uint32_t s = sv[u];
+            xp[u].x = __float_as_uint(w[u] * g_lds[s & 255u]);
+            xp[u].y = __float_as_uint(w[u] * g_lds[(s >> 8) & 255u]);
+            xp[u].z = __float_as_uint(w[u] * g_lds[(s >> 16) & 255u]);
+            xp[u].w = __float_as_uint(w[u] * g_lds[s >> 24]);
+            op[u] = (e < se && qok) ? (uint32_t)((e - sb) * k + 4 * q) * 4u : kDrop;
+        }
+        pending = true;
+        if (!has_next) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            c[u] = cn[u];
+            w[u] = wn[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(xp[u], rsrc, (int)op[u], 0, MAXK_T_AUX);
+}
 
 // Walk edges [sb, se) (sb < se) of one staged row.  All loads are
 // unconditional (clamped addresses).
@@ -43,6 +131,10 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
                                            const uint8_t *__restrict__ cbsr_idx,
                                            float *__restrict__ dst, int dummy, int sb, int se,
                                            int k, int lane) {
+    if constexpr (MODE == kStoreX4) {
+        push_x4<KG, U>(g_lds, col_idx, edge_val, cbsr_idx, dst, sb, se, k, lane);
+        return;
+    }
     constexpr int G = kWave / KG;
     constexpr int GU = G * U;
     const int grp = lane / KG;
@@ -54,8 +146,8 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
     for (int u = 0; u < U; ++u) {
         const int e = sb + u * G + grp;
         const int ec = e < se ? e : last;
-        c[u] = col_idx[ec];
-        w[u] = edge_val[ec];
+        c[u] = ld_stream(col_idx + ec);
+        w[u] = ld_stream(edge_val + ec);
     }
     if (MODE == kStore && k <= KG) {
         const bool lok = l0 < k;
@@ -72,8 +164,8 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
                 for (int u = 0; u < U; ++u) {
                     const int e = base + GU + u * G + grp;
                     const int ec = e < se ? e : last;
-                    cn[u] = col_idx[ec];
-                    wn[u] = edge_val[ec];
+                    cn[u] = ld_stream(col_idx + ec);
+                    wn[u] = ld_stream(edge_val + ec);
                 }
             }
             int s[U];
@@ -138,8 +230,8 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
         for (int u = 0; u < U; ++u) {
             const int e = base + GU + u * G + grp;
             const int ec = e < se ? e : last;
-            c[u] = col_idx[ec];
-            w[u] = edge_val[ec];
+            c[u] = ld_stream(col_idx + ec);
+            w[u] = ld_stream(edge_val + ec);
         }
     }
 }
@@ -229,8 +321,8 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t t = base + u * RI + g;
-                const int e = eid[t < te ? t : tb];
-                v[u] = T4[(size_t)(uint32_t)e * LR + q];
+                const int e = ld_stream(eid + (t < te ? t : tb));
+                v[u] = ld_trow(T4 + (size_t)(uint32_t)e * LR + q);
                 if (t >= te) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
@@ -260,8 +352,8 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int64_t t = base + u * G + grp;
-                    const int e = eid[t < te ? t : tb];
-                    v[u] = T[(size_t)(uint32_t)e * k + lc];
+                    const int e = ld_stream(eid + (t < te ? t : tb));
+                    v[u] = ld_trow(T + (size_t)(uint32_t)e * k + lc);
                     if (t >= te) v[u] = 0.f;
                 }
 #pragma unroll
@@ -284,7 +376,8 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
                                                          int chunk, int n_items) {
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int item = blockIdx.x * kWavesPerBlock + wid;
+    const int blk = MAXK_XCD_SUM ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int item = blk * kWavesPerBlock + wid;
     if (item >= n_items) return;
     const int64_t total = (int64_t)num_cols + num_e;
     const int64_t d0 = (int64_t)item * chunk;
@@ -349,6 +442,29 @@ int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 int chunk) {
     const int n_items = n_items_for(nr, num_e, chunk);
     const dim3 grid((unsigned)ceil_div(n_items, kWavesPerBlock));
+    if (MODE == kStore && MAXK_BWD_X4 && k % 4 == 0) {
+        switch (lanes_per_edge(k / 4)) {
+#define MAXK_CASE(LRV)                                                                       \
+    case LRV:                                                                                \
+        hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, MAXK_X4_U, kStoreX4>), grid, dim3(kBlock), \
+                           0, s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,   \
+                           nr, num_e, D, k, chunk, n_items);                                 \
+        break;
+            MAXK_CASE(1)
+            MAXK_CASE(2)
+            MAXK_CASE(4)
+            MAXK_CASE(8)
+            MAXK_CASE(16)
+            MAXK_CASE(32)
+            MAXK_CASE(64)
+#undef MAXK_CASE
+            default:
+                set_error("unsupported lane group");
+                return MAXK_ERR_INVALID;
+        }
+        MAXK_LAUNCHED("sspmm_bwd_kernel");
+        return MAXK_OK;
+    }
     switch (lanes_per_edge(k)) {
 #define MAXK_CASE(KGV)                                                                        \
     case KGV:                                                                                 \
@@ -478,7 +594,9 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
                                          k, bwd_chunk(num_rows, num_e, chunk_edges)))
             return rc;
     }
-    const dim3 grid((unsigned)ceil_div(L.n_items, kWavesPerBlock));
+    const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
+    const dim3 grid((unsigned)(MAXK_XCD_SUM ? xcd_grid(blocks) : blocks));
+    const dim3 fix_grid((unsigned)blocks);
     const int nc = (int)num_cols;
     if (vec_sum(k)) {
         hipLaunchKernelGGL((csc_sum_kernel<true, 64>), grid, dim3(kBlock), 0, s, col_ptr, csc_eid, T,
@@ -505,7 +623,7 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
         }
     }
     MAXK_LAUNCHED("csc_sum_kernel");
-    hipLaunchKernelGGL(csc_sum_fixup_kernel, grid, dim3(kBlock), 0, s, slab, slab_row, grad_cbsr,
+    hipLaunchKernelGGL(csc_sum_fixup_kernel, fix_grid, dim3(kBlock), 0, s, slab, slab_row, grad_cbsr,
                        k, L.n_items);
     MAXK_LAUNCHED("csc_sum_fixup_kernel");
     return MAXK_OK;
