@@ -20,6 +20,7 @@ forward and a reduce-scatter of the CBSR-gradient partials after the backward
 from __future__ import annotations
 
 import argparse
+import warnings
 import json
 import os
 import sys
@@ -31,6 +32,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spgemm-prunning_amd"))
 
+warnings.filterwarnings("ignore", message="Sparse CSR tensor support")
 METRIC = "SpGEMM+SSpMM GTEPS (edges/s) & HBM-BW% on Reddit h=256 k=16; vs CPU SpMM"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -154,6 +156,50 @@ def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
     }
 
 
+def cpu_spmm_baselines(row_ptr, col, val, dense, target_s=6.0):
+    """The reference's CPU SpMM denominators: scipy.sparse CSR @ dense X^ on
+    1 thread, and torch.sparse CSR mm on all host threads, each on a leading-row sample of
+    the same graph sized for ~target_s seconds.  X^ = the scattered top-k input [V, D]."""
+    import scipy.sparse as sp
+    rp = row_ptr.cpu().numpy().astype(np.int64)
+    c, v, X = col.cpu().numpy(), val.cpu().numpy(), dense.cpu().numpy()
+    E = int(rp[-1])
+    out = {}
+
+    def sample_rows(time_fn):
+        r = int(np.searchsorted(rp, max(1, E // 200)))
+        r = max(1, min(r, len(rp) - 1))
+        t = time_fn(r)
+        per_edge = t / max(1, int(rp[r]))
+        r1 = int(np.searchsorted(rp, min(E, int(target_s / per_edge))))
+        r1 = max(1, min(r1, len(rp) - 1))
+        return r1, time_fn(r1)
+
+    def scipy_run(r1):
+        A = sp.csr_matrix((v[:rp[r1]], c[:rp[r1]], rp[:r1 + 1]), shape=(r1, X.shape[0]))
+        t0 = time.perf_counter()
+        A @ X
+        return time.perf_counter() - t0
+
+    r1, t = sample_rows(scipy_run)
+    out["cpu_spmm_scipy"] = {"value": round(int(rp[r1]) / t / 1e9, 6), "unit": "GTEPS (fwd SpMM)",
+                             "cores": 1, "sample": f"rows [0,{r1}) = {int(rp[r1])} edges, {t:.2f}s"}
+    Xt = torch.from_numpy(X)
+
+    def torch_run(r1):
+        A = torch.sparse_csr_tensor(torch.from_numpy(rp[:r1 + 1]), torch.from_numpy(c[:rp[r1]]).long(),
+                                    torch.from_numpy(v[:rp[r1]]), (r1, X.shape[0]))
+        t0 = time.perf_counter()
+        A @ Xt
+        return time.perf_counter() - t0
+
+    r1, t = sample_rows(torch_run)
+    out["cpu_spmm_torch"] = {"value": round(int(rp[r1]) / t / 1e9, 6), "unit": "GTEPS (fwd SpMM)",
+                             "cores": torch.get_num_threads(),
+                             "sample": f"rows [0,{r1}) = {int(rp[r1])} edges, {t:.2f}s"}
+    return out
+
+
 # --------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -169,6 +215,9 @@ def main():
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--bwd-mode", default="csc", choices=["csc", "atomic"])
+    ap.add_argument("--graph-dir", default=None,
+                    help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
+    ap.add_argument("--no-cpu-spmm", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,7 +240,17 @@ def main():
     V = P["V"]
     E_target = P["E"] - ((P["E"] - V) % 2)
     t0 = time.time()
-    row_ptr, col = make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
+    import maxk_graph
+    gdir = maxk_graph.find_graph(args.graph, [args.graph_dir] if args.graph_dir else [])
+    if gdir:
+        g = maxk_graph.GraphDataLoader(gdir).load_graph(args.graph)
+        row_ptr = torch.from_numpy(g["indptr"]).to(dev)
+        col = torch.from_numpy(g["indices"]).to(dev)
+        V = g["v_num"]
+        data = f"real graph {gdir}/{args.graph}.indptr|.indices; synthetic features"
+    else:
+        row_ptr, col = make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
+        data = "synthetic"
     E = col.numel()
     gen = torch.Generator(device=dev).manual_seed(123)  # kernels/main.cu:74-77 seed
     val = torch.rand(E, generator=gen, device=dev)
@@ -346,15 +405,17 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(row_ptr, col, val, cv_all, ci_all, G, D, args.cpu_seconds)
+        if not args.no_cpu_spmm:
+            extra.update(cpu_spmm_baselines(row_ptr, col, val, mk.cbsr_scatter_dense(cv_all, ci_all, D)))
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 4), "unit": "GTEPS", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic",
+            "data": data,
             "config": {
-                "workload": (f"{args.graph}-synthetic fwd SpGEMM + bwd SSpMM, V={V} E={E} D={D} "
+                "workload": (f"{args.graph}-{'real' if gdir else 'synthetic'} fwd SpGEMM + bwd SSpMM, V={V} E={E} D={D} "
                              f"k={k}"),
                 "graph": args.graph, "V": V, "E": E, "D": D, "k": k,
                 "parallelism": f"vertex-range x{world}" if world > 1 else "single-gpu",

@@ -51,6 +51,12 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #ifndef MAXK_NT_TLOAD  // non-temporal loads of the contribution rows in phase 2
 #define MAXK_NT_TLOAD 0
 #endif
+#ifndef MAXK_TOPK_RADIX  // top-k threshold by 8-bit radix select (else bit construction)
+#define MAXK_TOPK_RADIX 1
+#endif
+#ifndef MAXK_TOPK_BLOCKS  // grid cap of the grid-stride top-k (rows per wave grow past it)
+#define MAXK_TOPK_BLOCKS 16384
+#endif
 #ifndef MAXK_SUM_U
 #define MAXK_SUM_U 8
 #endif

@@ -8,8 +8,10 @@
 // One wavefront per row (D <= 256, so <= 4 elements per lane, column
 // j = lane + 64*i for coalesced loads):
 //  1. order-preserving 32-bit keys (NaN above +inf, as torch ranks it);
-//  2. the k-th largest key T by MSB-first bit construction, each bit one
-//     ballot/popcount per element slot -- no LDS, no sorting of all D;
+//  2. the k-th largest key T by MSB-first radix select over 8-bit digits
+//     (per-wave 256-bin LDS histogram + wave suffix scan; 4 passes for f32).
+//     The earlier bit-by-bit construction (32 dependent ballot/popcount
+//     rounds, MAXK_TOPK_RADIX=0) was bound by the CU's shared scalar unit;
 //  3. select key > T, plus the lowest-column key == T until k are taken;
 //  4. compact the k winners into LDS, rank each against the others
 //     (broadcast LDS reads) and store in (key desc, column asc) order.
@@ -40,28 +42,103 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
                                                            uint8_t *__restrict__ out_idx,
                                                            int32_t *__restrict__ out_idx32,
                                                            int num_rows, int D, int k) {
-    __shared__ uint32_t s_key[kWavesPerBlock][kMaxDim];
-    __shared__ T s_val[kWavesPerBlock][kMaxDim];
-    __shared__ uint8_t s_col[kWavesPerBlock][kMaxDim];
+    // winner slots [0, k), padding slots [k, k4) (key 0, column 255: never ranked above a
+    // winner), and per-lane scratch slots [kMaxDim, kMaxDim + 64) for lanes not taking
+    constexpr int kSlots = kMaxDim + kWave;
+    __shared__ __attribute__((aligned(16))) uint32_t s_key[kWavesPerBlock][kSlots];
+    __shared__ T s_val[kWavesPerBlock][kSlots];
+    __shared__ __attribute__((aligned(16))) uint8_t s_col[kWavesPerBlock][kSlots];
+#if MAXK_TOPK_RADIX
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[kWavesPerBlock][256];
+#endif
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int row = blockIdx.x * kWavesPerBlock + wid;
-    if (row >= num_rows) return;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
-
+    const int stride = gridDim.x * kWavesPerBlock;
+    bool ok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ok[i] = lane + kWave * i < D;
+    // grid-stride over rows (a launch of one tiny workgroup per 4 rows is bound by the
+    // workgroup dispatch rate); the next row's values are loaded before this row is ranked
+    // loads are unconditional (clamped row / column), masked after: no predicated loads
+    int col4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) col4[i] = ok[i] ? lane + kWave * i : D - 1;
+    int row = blockIdx.x * kWavesPerBlock + wid;
+    T vn[4];
+    {
+        const T *xr = x + (int64_t)(row < num_rows ? row : num_rows - 1) * ld_x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vn[i] = xr[col4[i]];
+    }
+    for (; row < num_rows; row += stride) {
     T v[4];
     uint32_t key[4];
-    bool ok[4];
-    const T *xr = x + (int64_t)row * ld_x;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int j = lane + kWave * i;
-        ok[i] = j < D;
-        v[i] = ok[i] ? xr[j] : T(0);
+        v[i] = ok[i] ? vn[i] : T(0);
         key[i] = ok[i] ? order_key(v[i]) : 0u;
+    }
+    const int nrow = row + stride;
+    {
+        const T *xr = x + (int64_t)(nrow < num_rows ? nrow : row) * ld_x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vn[i] = xr[col4[i]];
     }
 
     // T = max t such that #{key >= t} >= k  (the k-th largest key)
+#if MAXK_TOPK_RADIX
+    // MSB-first radix select, 8-bit digits: per pass a 256-bin histogram of the keys
+    // still matching the chosen prefix (integer LDS atomics), a wave suffix scan of the
+    // bins, and the largest digit whose suffix count still reaches `need`.
+    uint32_t thr = 0, pmask = 0;
+    int need = k;  // how many of the keys matching the prefix are still to be taken
+    int sh = 0;    // selection compares key >> sh with thr >> sh (sh > 0 after an early exit)
+    uint32_t *hist = s_hist[wid];
+#if MAXK_TOPK_ABLATE & 2
+    for (int shift = -8; shift >= 0; shift -= 8) {
+#else
+    for (int shift = KeyBits<T>::value - 8; shift >= 0; shift -= 8) {
+#endif
+        reinterpret_cast<uint4 *>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+        wave_lds_fence();
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // branch-free: non-matching keys add 0
+            atomicAdd(&hist[(key[i] >> shift) & 255u], (ok[i] && (key[i] & pmask) == thr) ? 1u : 0u);
+        wave_lds_fence();
+        const uint4 h = reinterpret_cast<const uint4 *>(hist)[lane];  // bins 4*lane .. 4*lane+3
+        const uint32_t s3 = h.w, s2 = h.z + s3, s1 = h.y + s2, s0 = h.x + s1;
+        uint32_t acc = s0;  // -> sum of s0 over lanes >= this one
+#pragma unroll
+        for (int off = 1; off < kWave; off <<= 1) {
+            const uint32_t t = __shfl_down(acc, off);
+            acc += lane + off < kWave ? t : 0u;
+        }
+        const uint32_t above = acc - s0;  // keys with a digit in a higher lane's bins
+        const uint32_t nd = (uint32_t)need;
+        // largest digit d with #{digit >= d} >= need: the highest lane holding one
+        // (s0 >= s1 >= s2 >= s3: the conditions are monotone, m = their count - 1)
+        const int m = (int)(above + s0 >= nd) + (int)(above + s1 >= nd) +
+                      (int)(above + s2 >= nd) + (int)(above + s3 >= nd) - 1;
+        const uint32_t gt_l = above + (uint32_t)(m == 0) * s1 + (uint32_t)(m == 1) * s2 +
+                              (uint32_t)(m == 2) * s3;  // #{digit > 4*lane + m}
+        const uint32_t ge_l = above + (uint32_t)(m == 0) * s0 + (uint32_t)(m == 1) * s1 +
+                              (uint32_t)(m == 2) * s2 + (uint32_t)(m == 3) * s3;
+        const uint64_t has = __ballot(m >= 0);
+        const int src = 63 - __clzll(has);
+        const int dm = __shfl(m, src);
+        const uint32_t gt = __shfl(gt_l, src);
+        const uint32_t in_bin = __shfl(ge_l, src) - gt;
+        need -= (int)gt;
+        thr |= (uint32_t)(4 * src + dm) << shift;
+        pmask |= 255u << shift;
+        sh = shift;
+        if (in_bin == (uint32_t)need) break;  // the whole bin is taken: no lower digit matters
+    }
+    const int need_eq = need;
+    thr >>= sh;
+#else
+    const int sh = 0;
     uint32_t thr = 0;
     for (int bit = KeyBits<T>::value - 1; bit >= 0; --bit) {
         const uint32_t cand = thr | (1u << bit);
@@ -74,38 +151,53 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
 #pragma unroll
     for (int i = 0; i < 4; ++i) n_gt += __popcll(__ballot(ok[i] && key[i] > thr));
     const int need_eq = k - n_gt;
+#endif
 
     // select, then compact winners into LDS slots [0, k)
+    const int k4 = (k + 3) & ~3;
+    for (int p = k + lane; p < k4; p += kWave) {
+        s_key[wid][p] = 0u;
+        s_col[wid][p] = 255;
+    }
     int eq_base = 0, slot_base = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const bool eq = ok[i] && key[i] == thr;
+        const bool eq = ok[i] && (key[i] >> sh) == thr;
         const uint64_t me = __ballot(eq);
         const int eq_rank = eq_base + __popcll(me & lt_mask);
         eq_base += __popcll(me);
-        const bool take = (ok[i] && key[i] > thr) || (eq && eq_rank < need_eq);
+        const bool take = (ok[i] && (key[i] >> sh) > thr) || (eq && eq_rank < need_eq);
         const uint64_t mt = __ballot(take);
-        if (take) {
-            const int slot = slot_base + __popcll(mt & lt_mask);
-            s_key[wid][slot] = key[i];
-            s_val[wid][slot] = v[i];
-            s_col[wid][slot] = (uint8_t)(lane + kWave * i);
-        }
+        const int slot = take ? slot_base + __popcll(mt & lt_mask) : kMaxDim + lane;
+        s_key[wid][slot] = key[i];
+        s_val[wid][slot] = v[i];
+        s_col[wid][slot] = (uint8_t)(lane + kWave * i);
         slot_base += __popcll(mt);
     }
     wave_lds_fence();
+    // rank of winner p among the winners: (key desc, column asc); 4 slots per LDS read
     for (int p = lane; p < k; p += kWave) {
         const uint32_t kp = s_key[wid][p];
         const int cp = s_col[wid][p];
         int pos = 0;
-        for (int q = 0; q < k; ++q) {
-            const uint32_t kq = s_key[wid][q];
-            pos += (kq > kp) || (kq == kp && (int)s_col[wid][q] < cp);
+#if MAXK_TOPK_ABLATE & 1
+        pos = p;
+#else
+        for (int q = 0; q < k4; q += 4) {
+            const uint4 kq = *reinterpret_cast<const uint4 *>(&s_key[wid][q]);
+            const uint32_t cq = *reinterpret_cast<const uint32_t *>(&s_col[wid][q]);
+            pos += (kq.x > kp) || (kq.x == kp && (int)(cq & 255u) < cp);
+            pos += (kq.y > kp) || (kq.y == kp && (int)((cq >> 8) & 255u) < cp);
+            pos += (kq.z > kp) || (kq.z == kp && (int)((cq >> 16) & 255u) < cp);
+            pos += (kq.w > kp) || (kq.w == kp && (int)(cq >> 24) < cp);
         }
+#endif
         const int64_t o = (int64_t)row * k + pos;
         out_val[o] = s_val[wid][p];
         out_idx[o] = (uint8_t)cp;
         if (out_idx32) out_idx32[o] = cp;
+    }
+    wave_lds_fence();  // this row's LDS slots are read before the next row overwrites them
     }
 }
 
@@ -142,7 +234,8 @@ int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, 
     MAXK_REQUIRE(ld_x >= D, "ld_x (%lld) < dim_origin (%d)", (long long)ld_x, D);
     if (num_rows == 0) return MAXK_OK;
     MAXK_REQUIRE(x && val && idx, "x/val/idx must not be NULL");
-    const dim3 grid((unsigned)ceil_div(num_rows, kWavesPerBlock));
+    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
+    const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
     hipLaunchKernelGGL(topk_cbsr_kernel<T>, grid, dim3(kBlock), 0, as_stream(stream), x, ld_x, val,
                        idx, idx32, (int)num_rows, D, k);
     MAXK_LAUNCHED("topk_cbsr_kernel");

@@ -1,0 +1,130 @@
+"""On-disk graph format and preprocessing for the MaxK aggregation.
+
+Format (the reference's, kernels/main.cu `cuda_read_array`, graph_loader.py:19-85,
+dataset_gen.py:104-115): `<dir>/<name>.indptr` and `<dir>/<name>.indices`, raw
+little-endian int32 arrays of the CSR (V+1 and E entries), no header.
+
+`GraphDataLoader` keeps the reference loader's API (graph_loader.py:13-107): same
+method names, same returned keys, same synthetic edge weights (numpy seed 123,
+U(0,1) float32).  `build_csr` restates dataset_gen.py:59-104 (make undirected ->
+add a self loop on every vertex -> drop multi-edges -> CSR) as device-side
+sorts instead of a Python set loop, so the real Reddit / ogbn-products /
+ogbn-proteins graphs can be prepared on the GPU box in seconds; its output has
+sorted column indices, which the reference's DGL `adj_tensors('csr')` does not
+promise (the kernels accept either).
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+
+def read_binary_array(filepath: str, dtype=np.int32) -> np.ndarray:
+    """graph_loader.py:19-38: the whole file as one array."""
+    if not os.path.exists(filepath):
+        raise FileNotFoundError(f"Graph file not found: {filepath}")
+    if dtype not in (np.int32, np.float32):
+        raise ValueError(f"Unsupported dtype: {dtype}")
+    if os.path.getsize(filepath) % 4:
+        raise ValueError(f"{filepath}: size is not a multiple of 4 bytes")
+    return np.fromfile(filepath, dtype=dtype)
+
+
+def edge_values(e_num: int, seed: int = 123) -> np.ndarray:
+    """graph_loader.py:69-71: np.random.seed(123); U(0,1) float32 per edge."""
+    np.random.seed(seed)
+    return np.random.uniform(0, 1, e_num).astype(np.float32)
+
+
+def validate_csr(indptr: np.ndarray, indices: np.ndarray) -> None:
+    """Structural checks the reference skips: monotone indptr from 0 to E, columns in range."""
+    if indptr.ndim != 1 or indptr.size < 1:
+        raise ValueError("indptr must be a non-empty 1-D array")
+    if int(indptr[0]) != 0 or int(indptr[-1]) != indices.size:
+        raise ValueError(f"indptr must run from 0 to E={indices.size}")
+    if indptr.size > 1 and (np.diff(indptr) < 0).any():
+        raise ValueError("indptr must be non-decreasing")
+    V = indptr.size - 1
+    if indices.size and (int(indices.min()) < 0 or int(indices.max()) >= V):
+        raise ValueError(f"indices out of range [0, {V})")
+
+
+class GraphDataLoader:
+    """Reference-compatible loader (graph_loader.py:13): base_dir/<stem>.indptr|.indices."""
+
+    def __init__(self, base_dir: str = "kernels/graphs/"):
+        self.base_dir = base_dir
+
+    def read_binary_array(self, filepath, dtype=np.int32):
+        return read_binary_array(filepath, dtype)
+
+    def load_graph(self, graph_name: str, validate: bool = True) -> Dict:
+        stem = Path(graph_name).stem
+        indptr = read_binary_array(os.path.join(self.base_dir, f"{stem}.indptr"))
+        indices = read_binary_array(os.path.join(self.base_dir, f"{stem}.indices"))
+        if validate:
+            validate_csr(indptr, indices)
+        v_num, e_num = indptr.size - 1, indices.size
+        return {"graph_name": stem, "indptr": indptr, "indices": indices,
+                "values": edge_values(e_num), "v_num": v_num, "e_num": e_num}
+
+    def to_cuda_tensors(self, graph_data: Dict, device="cuda") -> Dict:
+        """graph_loader.py:87-100."""
+        out = {}
+        for key, value in graph_data.items():
+            out[key] = torch.from_numpy(np.ascontiguousarray(value)).to(device) \
+                if isinstance(value, np.ndarray) else value
+        return out
+
+
+def build_csr(src: torch.Tensor, dst: torch.Tensor, num_nodes: int, symmetrize: bool = True,
+              self_loops: bool = True, dedupe: bool = True):
+    """dataset_gen.py:59-104 on the tensors' device: edges (src -> dst) -> CSR rows = src.
+
+    Returns (indptr int32 [V+1], indices int32 [E]) with columns sorted within each row."""
+    src = src.to(torch.int64).flatten()
+    dst = dst.to(torch.int64).flatten()
+    if src.numel() != dst.numel():
+        raise ValueError("src and dst must have the same length")
+    V = int(num_nodes)
+    if src.numel() and (int(torch.minimum(src.min(), dst.min())) < 0 or
+                        int(torch.maximum(src.max(), dst.max())) >= V):
+        raise ValueError(f"edge endpoints out of range [0, {V})")
+    if symmetrize:                      # :61-66 add reverse edges
+        src, dst = torch.cat([src, dst]), torch.cat([dst, src])
+    if self_loops:                      # :75-76 dgl.add_self_loop: one more per vertex
+        loops = torch.arange(V, device=src.device)
+        src, dst = torch.cat([src, loops]), torch.cat([dst, loops])
+    key = src * V + dst
+    key = torch.unique(key) if dedupe else torch.sort(key).values  # :82-101 multi-edges
+    src, dst = key // V, key % V
+    indptr = torch.zeros(V + 1, dtype=torch.int64, device=key.device)
+    indptr[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)
+    return indptr.to(torch.int32), dst.to(torch.int32)
+
+
+def save_graph(indptr, indices, out_dir: str, name: str) -> None:
+    """dataset_gen.py:106-115: raw int32 files <out_dir>/<name>.indptr / .indices."""
+    os.makedirs(out_dir, exist_ok=True)
+    ip = indptr.cpu().numpy() if torch.is_tensor(indptr) else np.asarray(indptr)
+    ix = indices.cpu().numpy() if torch.is_tensor(indices) else np.asarray(indices)
+    ip.astype(np.int32).tofile(os.path.join(out_dir, f"{name}.indptr"))
+    ix.astype(np.int32).tofile(os.path.join(out_dir, f"{name}.indices"))
+
+
+def find_graph(name: str, dirs=None) -> Optional[str]:
+    """First directory holding <name>.indptr and <name>.indices (the reference keeps them under
+    kernels/graphs/ or ./processed_graphs/; MAXK_GRAPH_DIR adds one)."""
+    dirs = list(dirs or [])
+    if os.environ.get("MAXK_GRAPH_DIR"):
+        dirs.insert(0, os.environ["MAXK_GRAPH_DIR"])
+    dirs += ["kernels/graphs", "processed_graphs", "graphs"]
+    for d in dirs:
+        if os.path.exists(os.path.join(d, f"{name}.indptr")) and \
+                os.path.exists(os.path.join(d, f"{name}.indices")):
+            return d
+    return None

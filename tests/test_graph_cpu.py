@@ -1,0 +1,96 @@
+"""On-disk graph format + preprocessing (maxk_graph), against the reference's semantics
+(dataset_gen.py:59-115, graph_loader.py:19-85) restated as plain Python sets here."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import conftest  # noqa: F401  (sys.path)
+import maxk_graph as mg
+
+
+def _reference_edges(src, dst, V):
+    """dataset_gen.py:59-101: reverse edges added, a self loop on every vertex, duplicates
+    dropped (the reference's edge_set loop)."""
+    s = list(src) + list(dst) + list(range(V))
+    d = list(dst) + list(src) + list(range(V))
+    return sorted(set(zip(s, d)))
+
+
+def _csr_edges(indptr, indices):
+    indptr, indices = np.asarray(indptr), np.asarray(indices)
+    rows = np.repeat(np.arange(indptr.size - 1), np.diff(indptr))
+    return list(zip(rows.tolist(), indices.tolist()))
+
+
+@pytest.mark.parametrize("V,m,seed", [(1, 0, 0), (7, 20, 1), (300, 2000, 2)])
+def test_build_csr_matches_reference_pipeline(V, m, seed):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, V, m)
+    dst = rng.integers(0, V, m)
+    if m:
+        src[:3], dst[:3] = src[0], dst[0]  # multi-edges
+        dst[3] = src[3]                    # an existing self loop
+    indptr, indices = mg.build_csr(torch.from_numpy(src), torch.from_numpy(dst), V)
+    assert indptr.dtype == torch.int32 and indices.dtype == torch.int32
+    assert _csr_edges(indptr, indices) == _reference_edges(src.tolist(), dst.tolist(), V)
+    # columns sorted inside each row, every vertex has its self loop
+    ip, ix = indptr.numpy(), indices.numpy()
+    for r in range(V):
+        row = ix[ip[r]:ip[r + 1]]
+        assert (np.diff(row) > 0).all() and r in row
+
+
+def test_build_csr_options():
+    src = torch.tensor([0, 0, 2])
+    dst = torch.tensor([1, 1, 0])
+    ip, ix = mg.build_csr(src, dst, 3, symmetrize=False, self_loops=False, dedupe=False)
+    assert _csr_edges(ip, ix) == [(0, 1), (0, 1), (2, 0)]
+    ip, ix = mg.build_csr(src, dst, 3, symmetrize=False, self_loops=False)
+    assert _csr_edges(ip, ix) == [(0, 1), (2, 0)]
+    with pytest.raises(ValueError):
+        mg.build_csr(torch.tensor([0]), torch.tensor([3]), 3)
+
+
+def test_save_load_roundtrip(tmp_path):
+    rng = np.random.default_rng(5)
+    ip, ix = mg.build_csr(torch.from_numpy(rng.integers(0, 50, 400)),
+                          torch.from_numpy(rng.integers(0, 50, 400)), 50)
+    mg.save_graph(ip, ix, str(tmp_path), "toy")
+    # raw int32 files, no header (dataset_gen.py:109-110)
+    assert os.path.getsize(tmp_path / "toy.indptr") == 4 * 51
+    assert os.path.getsize(tmp_path / "toy.indices") == 4 * ix.numel()
+    g = mg.GraphDataLoader(str(tmp_path)).load_graph("toy.dgl")  # extension stripped (:49)
+    assert g["graph_name"] == "toy" and g["v_num"] == 50 and g["e_num"] == ix.numel()
+    np.testing.assert_array_equal(g["indptr"], ip.numpy())
+    np.testing.assert_array_equal(g["indices"], ix.numpy())
+    np.random.seed(123)
+    np.testing.assert_array_equal(g["values"],
+                                  np.random.uniform(0, 1, ix.numel()).astype(np.float32))
+    t = mg.GraphDataLoader(str(tmp_path)).to_cuda_tensors(g, device="cpu")
+    assert t["indptr"].dtype == torch.int32 and t["values"].dtype == torch.float32
+    assert mg.find_graph("toy", [str(tmp_path)]) == str(tmp_path)
+    assert mg.find_graph("missing", [str(tmp_path)]) is None
+
+
+def test_loader_errors(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        mg.GraphDataLoader(str(tmp_path)).load_graph("nope")
+    np.array([0, 2, 1], dtype=np.int32).tofile(tmp_path / "bad.indptr")
+    np.array([0, 1], dtype=np.int32).tofile(tmp_path / "bad.indices")
+    with pytest.raises(ValueError):
+        mg.GraphDataLoader(str(tmp_path)).load_graph("bad")
+    np.array([0, 1], dtype=np.int32).tofile(tmp_path / "oob.indptr")
+    np.array([7], dtype=np.int32).tofile(tmp_path / "oob.indices")
+    with pytest.raises(ValueError):
+        mg.GraphDataLoader(str(tmp_path)).load_graph("oob")
+
+
+@pytest.mark.gpu
+def test_build_csr_on_device_matches_cpu(cuda):
+    rng = np.random.default_rng(9)
+    src, dst = rng.integers(0, 5000, 60000), rng.integers(0, 5000, 60000)
+    a = mg.build_csr(torch.from_numpy(src), torch.from_numpy(dst), 5000)
+    b = mg.build_csr(torch.from_numpy(src).to(cuda), torch.from_numpy(dst).to(cuda), 5000)
+    assert torch.equal(a[0], b[0].cpu()) and torch.equal(a[1], b[1].cpu())
