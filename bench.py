@@ -225,12 +225,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # MAXK_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices, collectives
+    # staged through host); the default is RCCL with one rank per GPU.
+    backend = os.environ.get("MAXK_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev_idx = local_rank % ndev if backend == "gloo" else local_rank
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import maxk_cuda_kernels as mk
 
@@ -289,8 +297,8 @@ def main():
         gs_all = gs_loc = torch.empty(V, k, device=dev)
     y = torch.empty(nl, D, device=dev)
     if world > 1:
-        dist.all_gather_into_tensor(cv_all, cv_loc)
-        dist.all_gather_into_tensor(ci_all, ci_loc)
+        maxk_dist.all_gather_rows(cv_all, cv_loc)
+        maxk_dist.all_gather_rows(ci_all, ci_loc)
     # one validated call (row_ptr/col_idx/selector ranges) before the raw timed launches
     mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, validate=True)
     # per-graph setup (like the reference's warp4 files): transpose plan for the backward
@@ -305,8 +313,8 @@ def main():
 
     def step(ev=None):
         if world > 1:
-            dist.all_gather_into_tensor(cv_all, cv_loc)
-            dist.all_gather_into_tensor(ci_all, ci_loc)
+            maxk_dist.all_gather_rows(cv_all, cv_loc)
+            maxk_dist.all_gather_rows(ci_all, ci_loc)
         if ev:
             ev[0].record()
         mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, chunk=args.chunk,
@@ -318,7 +326,7 @@ def main():
         if ev:
             ev[2].record()
         if world > 1:
-            dist.reduce_scatter_tensor(gs_loc, gs_all)
+            maxk_dist.reduce_scatter_rows(gs_loc, gs_all)
 
     for _ in range(args.warmup):
         step()
@@ -335,7 +343,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -344,9 +352,25 @@ def main():
     b = (cv_all.double() * gs_all.double()).sum()
     if dist:
         ab = torch.stack([a, b])
+        if backend != "nccl":
+            ab = ab.cpu()
         dist.all_reduce(ab)
         a, b = ab[0], ab[1]
     adj_err = abs(float(a) - float(b)) / max(1.0, abs(float(a)))
+
+    if world > 1:
+        # every rank holds the whole graph and X/G (same seeds): recompute its rows unsharded
+        cv_f, ci_f = mk.topk_cbsr(X, k)
+        y_f = mk.spgemm_forward(row_ptr, col, val, cv_f, ci_f, D, validate=False)[v0:v1]
+        gs_f = mk.sspmm_backward(row_ptr, col, val, G, ci_f, validate=False,
+                                 mode=args.bwd_mode)[v0:v1]
+        errs = torch.tensor([
+            float(((y - y_f).abs() / y_f.abs().clamp(min=1)).max()) if nl else 0.0,
+            float(((gs_loc[:nl] - gs_f).abs() / gs_f.abs().clamp(min=1)).max()) if nl else 0.0],
+            dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(errs, op=dist.ReduceOp.MAX)
+        dist_err = [float(errs[0]), float(errs[1])]
+        del y_f, gs_f, cv_f, ci_f
 
     fwd_ms = [e[0].elapsed_time(e[1]) for e in evs]
     bwd_ms = [e[1].elapsed_time(e[2]) for e in evs]
@@ -369,6 +393,10 @@ def main():
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
         "bwd_mode": args.bwd_mode, "transpose_plan_s": round(t_plan, 4),
     }
+    if world > 1:
+        extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
+                      "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
+                      "rows_per_rank_max": vmax, "edges_this_rank0": El})
 
     if rank == 0 and world == 1:
         # CBSR encode (top-k) and the dense rocSPARSE SpMM denominator, outside the timed region

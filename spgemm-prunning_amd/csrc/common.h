@@ -39,8 +39,8 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #ifndef MAXK_BWD_X4  // 4-l-per-lane phase 1 of the two-phase backward (k % 4 == 0)
 #define MAXK_BWD_X4 1
 #endif
-#ifndef MAXK_X4_U
-#define MAXK_X4_U 16
+#ifndef MAXK_X4_U  // phase-1 depth; 0 = chosen per launch from the average degree
+#define MAXK_X4_U 0
 #endif
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
@@ -57,8 +57,11 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #ifndef MAXK_TOPK_BLOCKS  // grid cap of the grid-stride top-k (rows per wave grow past it)
 #define MAXK_TOPK_BLOCKS 16384
 #endif
-#ifndef MAXK_SUM_U
-#define MAXK_SUM_U 8
+#ifndef MAXK_BWD_ROWWIN  // phase 1: row_ptr/row_div window in registers + next-row G prefetch
+#define MAXK_BWD_ROWWIN 1
+#endif
+#ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
+#define MAXK_SUM_U 0
 #endif
 
 // ---- error reporting (host) ----

@@ -275,7 +275,55 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
     const int64_t d0 = (int64_t)item * chunk;
     const int64_t d1 = d0 + chunk < total ? d0 + chunk : total;
     int r = wave_first_row_token(row_ptr, num_rows, d0);
-
+#if MAXK_BWD_ROWWIN
+    // Rows q = r-1 (continuation), r, r+1, ...: the item's edges of row q are
+    // [max(rb, d0-q-1), min(re, d1-q-1)).  row_ptr / row_div of 64 consecutive rows sit
+    // one per lane (read with readlane), and each row's G values (4 per lane, columns
+    // lane + 64*i) are loaded while the previous row's edges are pushed: no per-row
+    // dependent load before a row can start.
+    int q = r > 0 ? r - 1 : 0;
+    int wb = q;
+    int rpw = row_ptr[wb + lane < num_rows ? wb + lane : num_rows];
+    float dvw = row_div ? row_div[wb + lane < num_rows ? wb + lane : num_rows - 1] : 1.f;
+    auto load_g = [&](int row, float (&g)[4]) {
+        const float *gr = grad + (int64_t)(row < num_rows ? row : num_rows - 1) * D;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = lane + kWave * i;
+            g[i] = gr[j < D ? j : D - 1];
+        }
+    };
+    float gn[4];
+    load_g(q, gn);
+    for (; q < num_rows; ++q) {
+        if (q + 1 - wb >= kWave) {  // slide the window
+            wb = q;
+            rpw = row_ptr[wb + lane < num_rows ? wb + lane : num_rows];
+            if (row_div) dvw = row_div[wb + lane < num_rows ? wb + lane : num_rows - 1];
+        }
+        const int rb = __builtin_amdgcn_readlane(rpw, q - wb);
+        const int re = __builtin_amdgcn_readlane(rpw, q + 1 - wb);
+        if ((int64_t)q + rb >= d1) break;
+        float g[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[i] = gn[i];
+        if (q + 1 < num_rows) load_g(q + 1, gn);
+        const int64_t sb64 = d0 - q - 1 > rb ? d0 - q - 1 : rb;
+        const int64_t se64 = d1 - q - 1 < re ? d1 - q - 1 : re;
+        if (sb64 >= se64) continue;
+        const float div = __builtin_bit_cast(
+            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, dvw), q - wb));
+        wave_lds_fence();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = lane + kWave * i;
+            if (j < D) g_lds[j] = row_div ? g[i] / div : g[i];
+        }
+        wave_lds_fence();
+        push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)sb64,
+                                (int)se64, k, lane);
+    }
+#else
     if (r > 0) {  // continuation of row r-1
         const int64_t sb = d0 - r;
         int64_t se = (int64_t)row_ptr[r];
@@ -298,6 +346,7 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
         push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)rb,
                                 (int)se, k, lane);
     }
+#endif
 }
 
 // ---- phase 2: grad_cbsr[c, :] = sum over the CSC slots t of c of T[eid[t], :] -------
@@ -306,11 +355,10 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
 // dst[0:k], in a fixed order.  VEC (k in {4,8,...,256}): LR = k/4 lanes per row
 // (16-B loads), 64/LR rows per wave step, U steps in flight; the row groups are
 // combined by xor butterflies.  Scalar: KG = pow2ceil(k) lanes per row.
-template <bool VEC, int KG>
+template <bool VEC, int KG, int U>
 __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
                                             const int32_t *__restrict__ eid, int64_t tb,
                                             int64_t te, int k, float *__restrict__ dst, int lane) {
-    constexpr int U = MAXK_SUM_U;
     if constexpr (VEC) {
         const int LR = k / 4, RI = kWave / LR;
         const int g = lane / LR, q = lane % LR;
@@ -365,7 +413,7 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
     }
 }
 
-template <bool VEC, int KG>
+template <bool VEC, int KG, int U>
 __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restrict__ col_ptr,
                                                          const int32_t *__restrict__ eid,
                                                          const float *__restrict__ T,
@@ -389,7 +437,7 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
         int64_t se = (int64_t)col_ptr[c];
         if (d1 - c < se) se = d1 - c;
         if (sb < se) {
-            segment_sum<VEC, KG>(T, eid, sb, se, k, slab + (int64_t)item * k, lane);
+            segment_sum<VEC, KG, U>(T, eid, sb, se, k, slab + (int64_t)item * k, lane);
             cont = c - 1;
         }
     }
@@ -399,7 +447,7 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
         if (cb + c >= d1) break;
         int64_t se = (int64_t)col_ptr[c + 1];
         if (d1 - c - 1 < se) se = d1 - c - 1;
-        segment_sum<VEC, KG>(T, eid, cb, se, k, grad_cbsr + (int64_t)c * k, lane);
+        segment_sum<VEC, KG, U>(T, eid, cb, se, k, grad_cbsr + (int64_t)c * k, lane);
     }
 }
 
@@ -435,6 +483,18 @@ int n_items_for(int64_t rows, int64_t num_e, int chunk) {
     return (int)(n > 0 ? n : 1);
 }
 
+// Loads in flight per lane ("depth" U): one wave step covers `per_step` edges (or
+// contribution rows), a batch U steps.  Deep batches keep more bytes in flight on long
+// rows; on short rows they are mostly masked lanes.  Largest U in [lo, hi] (powers of
+// two) whose batch still fits an average row (measured: products deg 50 -> 4, Reddit /
+// proteins deg 500-600 -> 16 for phase 1; 4 / 8 for phase 2).
+int pick_depth(int64_t num_e, int64_t rows, int per_step, int lo, int hi) {
+    const int64_t avg = rows > 0 ? num_e / rows : 0;
+    int u = lo;
+    while (u < hi && (int64_t)per_step * u * 2 <= avg) u <<= 1;
+    return u;
+}
+
 template <int MODE>
 int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 const float *edge_val, const float *grad, const float *row_div,
@@ -443,12 +503,23 @@ int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
     const int n_items = n_items_for(nr, num_e, chunk);
     const dim3 grid((unsigned)ceil_div(n_items, kWavesPerBlock));
     if (MODE == kStore && MAXK_BWD_X4 && k % 4 == 0) {
-        switch (lanes_per_edge(k / 4)) {
+        const int lr = lanes_per_edge(k / 4);
+        const int u = MAXK_X4_U > 0 ? MAXK_X4_U : pick_depth(num_e, nr, kWave / lr, 4, 16);
+        switch (lr) {
 #define MAXK_CASE(LRV)                                                                       \
     case LRV:                                                                                \
-        hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, MAXK_X4_U, kStoreX4>), grid, dim3(kBlock), \
-                           0, s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,   \
-                           nr, num_e, D, k, chunk, n_items);                                 \
+        if (u <= 4)                                                                          \
+            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 4, kStoreX4>), grid, dim3(kBlock), 0,  \
+                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
+                               nr, num_e, D, k, chunk, n_items);                             \
+        else if (u <= 8)                                                                     \
+            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 8, kStoreX4>), grid, dim3(kBlock), 0,  \
+                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
+                               nr, num_e, D, k, chunk, n_items);                             \
+        else                                                                                 \
+            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 16, kStoreX4>), grid, dim3(kBlock), 0, \
+                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
+                               nr, num_e, D, k, chunk, n_items);                             \
         break;
             MAXK_CASE(1)
             MAXK_CASE(2)
@@ -599,13 +670,24 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
     const dim3 fix_grid((unsigned)blocks);
     const int nc = (int)num_cols;
     if (vec_sum(k)) {
-        hipLaunchKernelGGL((csc_sum_kernel<true, 64>), grid, dim3(kBlock), 0, s, col_ptr, csc_eid, T,
-                           grad_cbsr, slab, slab_row, nc, num_e, k, L.chunk, L.n_items);
+        const int rows_per_step = kWave / (k / 4);
+        const int u = MAXK_SUM_U > 0 ? MAXK_SUM_U
+                                     : pick_depth(num_e, num_cols, rows_per_step, 2, 8);
+#define MAXK_SUM_LAUNCH(UV)                                                                  \
+    hipLaunchKernelGGL((csc_sum_kernel<true, 64, UV>), grid, dim3(kBlock), 0, s, col_ptr,    \
+                       csc_eid, T, grad_cbsr, slab, slab_row, nc, num_e, k, L.chunk, L.n_items)
+        if (u <= 2)
+            MAXK_SUM_LAUNCH(2);
+        else if (u <= 4)
+            MAXK_SUM_LAUNCH(4);
+        else
+            MAXK_SUM_LAUNCH(8);
+#undef MAXK_SUM_LAUNCH
     } else {
         switch (lanes_per_edge(k)) {
 #define MAXK_CASE(KGV)                                                                        \
     case KGV:                                                                                 \
-        hipLaunchKernelGGL((csc_sum_kernel<false, KGV>), grid, dim3(kBlock), 0, s, col_ptr,    \
+        hipLaunchKernelGGL((csc_sum_kernel<false, KGV, 4>), grid, dim3(kBlock), 0, s, col_ptr, \
                            csc_eid, T,                                                        \
                            grad_cbsr, slab, slab_row, nc, num_e, k, L.chunk, L.n_items);      \
         break;

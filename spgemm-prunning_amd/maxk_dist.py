@@ -30,6 +30,32 @@ import torch.distributed as dist
 from torch.autograd import Function
 
 
+def _staged(group) -> bool:
+    """gloo has no device collectives for these calls: stage through host memory (the CPU
+    tests, and rehearsing N ranks on a one-GPU box).  RCCL ("nccl") runs them on device."""
+    return dist.get_backend(group) == "gloo"
+
+
+def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """out[p * n:(p + 1) * n] = inp of rank p (equal n on every rank)."""
+    if _staged(group) and inp.is_cuda:
+        tmp = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(tmp, inp.cpu(), group=group)
+        out.copy_(tmp)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def reduce_scatter_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """out = sum over ranks of inp[rank * n:(rank + 1) * n]."""
+    if _staged(group) and inp.is_cuda:
+        tmp = torch.empty(out.shape, dtype=out.dtype)
+        dist.reduce_scatter_tensor(tmp, inp.cpu(), group=group)
+        out.copy_(tmp)
+    else:
+        dist.reduce_scatter_tensor(out, inp, group=group)
+
+
 def balanced_bounds(row_ptr: torch.Tensor, world: int) -> List[int]:
     """Row boundaries [0 = b0 <= b1 <= ... <= b_world = V] with ~E/world edges per shard."""
     rp = row_ptr.detach().to("cpu", torch.int64)
@@ -97,8 +123,8 @@ class ShardedMaxK:
         k = val_local.shape[1]
         val_all = torch.empty(self.n_cols, k, dtype=val_local.dtype, device=val_local.device)
         idx_all = torch.empty(self.n_cols, k, dtype=idx_local.dtype, device=idx_local.device)
-        dist.all_gather_into_tensor(val_all, self.pad_rows(val_local).contiguous(), group=self.group)
-        dist.all_gather_into_tensor(idx_all, self.pad_rows(idx_local).contiguous(), group=self.group)
+        all_gather_rows(val_all, self.pad_rows(val_local).contiguous(), self.group)
+        all_gather_rows(idx_all, self.pad_rows(idx_local).contiguous(), self.group)
         return val_all, idx_all
 
     def plan(self):
@@ -119,7 +145,7 @@ class ShardedMaxK:
                                               grad_local.contiguous(), idx_all,
                                               row_div=row_div_local, plan=self.plan())
         out = torch.empty(self.vmax, partial.shape[1], dtype=partial.dtype, device=partial.device)
-        dist.reduce_scatter_tensor(out, partial.contiguous(), group=self.group)
+        reduce_scatter_rows(out, partial.contiguous(), self.group)
         return out[:self.n_local]
 
 
