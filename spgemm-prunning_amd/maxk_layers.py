@@ -1,0 +1,208 @@
+"""MaxK-GNN layers on the drop-in aggregation, without DGL.
+
+The reference's integrated models (model_integrated_v3.py: OPTMaxK :28-43,
+MaxKSAGEConv :62-192, MaxKGraphConv :194-398, MaxKGINConv :400-520, MaxKSAGE
+:522-588) wrap DGL graphs; here a layer takes a `CSRGraph` (row r = destination,
+its columns = source vertices) and every aggregation goes through
+`maxk_spgemm_function.maxk_spgemm` (v4 shape) -> the HIP kernels.  The MaxK
+nonlinearity runs on the HIP top-k.
+
+Caller defects of the reference fixed here, each documented
+where it applies:
+  * OPTMaxK.backward drops the gradient of topk_values (:39-43) -> MaxK below
+    returns grad = scatter(gather(g_dense) + g_topk);
+  * GCN "both"/"left" normalisation scales feat_src, but the kernel is then fed
+    the unnormalised topk_values AND divides by degree (:301-310, 341-345,
+    380-389) -> here the symmetric normalisation is folded into the edge values
+    once per graph and the kernel divides by nothing;
+  * lin_before_mp paths apply the Linear to the [V, k] top-k values (:166, 330)
+    -> here aggregation always runs on the CBSR and the Linear after it (equal by
+    linearity, and the aggregation keeps its k-sparse input);
+  * GIN "sum" passes the degrees, i.e. computes a mean (:493) -> here a sum.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+from torch.autograd import Function
+
+import maxk_cuda_kernels as mk
+from maxk_spgemm_function import maxk_spgemm
+
+
+class CSRGraph:
+    """Adjacency in CSR with rows = destinations: out[r] aggregates x[indices[e]], e in row r."""
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor,
+                 values: Optional[torch.Tensor] = None):
+        self.indptr = indptr.int().contiguous()
+        self.indices = indices.int().contiguous()
+        self.num_nodes = self.indptr.numel() - 1
+        self.values = (torch.ones(self.indices.numel(), device=self.indices.device)
+                       if values is None else values.float().contiguous())
+        # in-degree of a destination row, out-degree of a source (column counts)
+        self.in_degrees = torch.diff(self.indptr).float()
+        self.out_degrees = torch.bincount(self.indices.long(),
+                                          minlength=self.num_nodes).float()
+        self._rows = None
+
+    def edge_rows(self) -> torch.Tensor:
+        if self._rows is None:
+            self._rows = torch.repeat_interleave(
+                torch.arange(self.num_nodes, device=self.indptr.device),
+                torch.diff(self.indptr).long())
+        return self._rows
+
+    def aggregate(self, topk_values, topk_indices, dim: int, values=None, row_div=None):
+        """(A . scatter(CBSR))[r] / row_div[r] through the drop-in v4 surface."""
+        return maxk_spgemm(self.indices, self.values if values is None else values,
+                           topk_values, topk_indices, None, 0, self.indptr, row_div,
+                           dim_origin=dim)
+
+
+class MaxK(Function):
+    """MaxK nonlinearity (model_integrated_v3.py:28-60): keeps the k largest entries of each
+    row.  Returns (dense masked output, topk_values, topk_indices u8); gradients from the
+    dense output and from topk_values both reach the input (the reference drops the latter)."""
+
+    @staticmethod
+    def forward(ctx, x: torch.Tensor, k: int):
+        x = x.float().contiguous()
+        vals, idx = mk.topk_cbsr(x, int(k))
+        dense = mk.cbsr_scatter_dense(vals, idx, x.shape[1])
+        ctx.save_for_backward(idx)
+        ctx.D = x.shape[1]
+        ctx.mark_non_differentiable(idx)
+        return dense, vals, idx
+
+    @staticmethod
+    def backward(ctx, g_dense, g_vals, g_idx):
+        idx, = ctx.saved_tensors
+        g = torch.zeros(idx.shape, device=idx.device) if g_vals is None else g_vals.float()
+        if g_dense is not None:
+            g = g + torch.gather(g_dense.float(), 1, idx.long())
+        return mk.cbsr_scatter_dense(g.contiguous(), idx, ctx.D), None
+
+
+def maxk(x: torch.Tensor, k: int):
+    return MaxK.apply(x, k)
+
+
+class MaxKSAGEConv(nn.Module):
+    """GraphSAGE-mean on MaxK features (model_integrated_v3.py:62-192):
+    rst = fc_self(x_sparse) + fc_neigh(mean_{u in N(v)} x_sparse[u])."""
+
+    def __init__(self, in_feats: int, out_feats: int, bias: bool = True, feat_drop: float = 0.,
+                 activation=None, norm: Optional[nn.Module] = None):
+        super().__init__()
+        self.in_feats, self.out_feats = in_feats, out_feats
+        self.fc_neigh = nn.Linear(in_feats, out_feats, bias=False)
+        self.fc_self = nn.Linear(in_feats, out_feats, bias=bias)
+        self.feat_drop = nn.Dropout(feat_drop)
+        self.activation, self.norm = activation, norm
+        gain = nn.init.calculate_gain("relu")
+        nn.init.xavier_uniform_(self.fc_self.weight, gain=gain)
+        nn.init.xavier_uniform_(self.fc_neigh.weight, gain=gain)
+
+    def forward(self, graph: CSRGraph, x_sparse, topk_values, topk_indices):
+        deg = graph.in_degrees.clamp(min=1.0)
+        h_neigh = self.fc_neigh(graph.aggregate(topk_values, topk_indices, self.in_feats,
+                                                row_div=deg))
+        rst = self.fc_self(self.feat_drop(x_sparse)) + h_neigh
+        if self.activation is not None:
+            rst = self.activation(rst)
+        if self.norm is not None:
+            rst = self.norm(rst)
+        return rst
+
+
+class MaxKGraphConv(nn.Module):
+    """GCN on MaxK features (model_integrated_v3.py:194-398): rst = (N A N') x_sparse W + b,
+    norm "both" = D_in^-1/2 A D_out^-1/2, "right" = D_in^-1 A, "left" = A D_out^-1."""
+
+    def __init__(self, in_feats: int, out_feats: int, norm: str = "both", weight: bool = True,
+                 bias: bool = True, activation=None):
+        super().__init__()
+        if norm not in ("none", "both", "right", "left"):
+            raise ValueError(f'Invalid norm value. Must be either "none", "both", "right" or '
+                             f'"left". But got "{norm}".')
+        self.in_feats, self.out_feats, self._norm = in_feats, out_feats, norm
+        self.weight = nn.Parameter(torch.empty(in_feats, out_feats)) if weight else None
+        self.bias = nn.Parameter(torch.zeros(out_feats)) if bias else None
+        self.activation = activation
+        if self.weight is not None:
+            nn.init.xavier_uniform_(self.weight)
+        self._graph_key = None
+        self._edge_values = None
+
+    def _norm_values(self, graph: CSRGraph) -> torch.Tensor:
+        if self._graph_key is not graph:  # once per graph, like the reference's set_graph_data
+            v = graph.values
+            if self._norm in ("left", "both"):
+                src = graph.out_degrees.clamp(min=1.0)
+                src = src.pow(-0.5) if self._norm == "both" else 1.0 / src
+                v = v * src[graph.indices.long()]
+            if self._norm in ("right", "both"):
+                dst = graph.in_degrees.clamp(min=1.0)
+                dst = dst.pow(-0.5) if self._norm == "both" else 1.0 / dst
+                v = v * dst[graph.edge_rows()]
+            self._edge_values, self._graph_key = v.contiguous(), graph
+        return self._edge_values
+
+    def forward(self, graph: CSRGraph, x_sparse, topk_values, topk_indices):
+        rst = graph.aggregate(topk_values, topk_indices, self.in_feats,
+                              values=self._norm_values(graph))
+        if self.weight is not None:
+            rst = rst @ self.weight
+        if self.bias is not None:
+            rst = rst + self.bias
+        if self.activation is not None:
+            rst = self.activation(rst)
+        return rst
+
+
+class MaxKGINConv(nn.Module):
+    """GIN-sum on MaxK features (model_integrated_v3.py:400-520):
+    rst = apply_func((1 + eps) x + sum_{u in N(v)} x_sparse[u])."""
+
+    def __init__(self, apply_func: Optional[nn.Module] = None, init_eps: float = 0.,
+                 learn_eps: bool = False, activation=None):
+        super().__init__()
+        self.apply_func, self.activation = apply_func, activation
+        if learn_eps:
+            self.eps = nn.Parameter(torch.tensor([float(init_eps)]))
+        else:
+            self.register_buffer("eps", torch.tensor([float(init_eps)]))
+
+    def forward(self, graph: CSRGraph, x, topk_values, topk_indices):
+        neigh = graph.aggregate(topk_values, topk_indices, x.shape[1])
+        rst = (1 + self.eps) * x + neigh
+        if self.apply_func is not None:
+            rst = self.apply_func(rst)
+        if self.activation is not None:
+            rst = self.activation(rst)
+        return rst
+
+
+class MaxKSAGE(nn.Module):
+    """lin_in -> [MaxK -> MaxKSAGEConv] x L -> lin_out (model_integrated_v3.py:522-588)."""
+
+    def __init__(self, in_size: int, hid_size: int, out_size: int, num_layers: int = 3,
+                 maxk: int = 32, feat_drop: float = 0., norm: bool = False):
+        super().__init__()
+        self.k = maxk
+        self.lin_in = nn.Linear(in_size, hid_size)
+        self.layers = nn.ModuleList([
+            MaxKSAGEConv(hid_size, hid_size, feat_drop=feat_drop,
+                         norm=nn.LayerNorm(hid_size) if norm else None)
+            for _ in range(num_layers)])
+        self.lin_out = nn.Linear(hid_size, out_size)
+
+    def forward(self, graph: CSRGraph, x):
+        x = self.lin_in(x)
+        for layer in self.layers:
+            x_sparse, vals, idx = maxk(x, self.k)
+            x = layer(graph, x_sparse, vals, idx)
+        return self.lin_out(x)
