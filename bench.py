@@ -31,19 +31,13 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spgemm-prunning_amd"))
+import maxk_graph  # noqa: E402
 
 warnings.filterwarnings("ignore", message="Sparse CSR tensor support")
 METRIC = "SpGEMM+SSpMM GTEPS (edges/s) & HBM-BW% on Reddit h=256 k=16; vs CPU SpMM"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
-# name: V, E (published sizes), power-law (alpha, offset) fitted so
-# the max/avg degree ratio resembles the real graph
-PRESETS = {
-    "reddit": dict(V=232_965, E=114_615_891, alpha=0.7, i0=200, D=256, k=16),
-    "products": dict(V=2_449_029, E=123_718_280, alpha=0.75, i0=3000, D=256, k=32),
-    "proteins": dict(V=132_534, E=79_122_504, alpha=0.45, i0=2000, D=256, k=64),
-    "flickr": dict(V=89_250, E=989_006, alpha=0.9, i0=30, D=64, k=16),
-}
+
 
 
 # kernels making up each op of one step (rocprofv3 names, maxk:: namespace)
@@ -70,44 +64,6 @@ def load_traffic(key, op):
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
-
-
-# --------------------------------------------------------------------------- synthetic graph
-def make_graph(V, E, alpha, i0, seed, device):
-    """Symmetric Chung-Lu power-law graph with self loops, deduplicated, CSR with sorted
-    columns (the shape dataset_gen.py:44-115 produces), exactly E edges when E-V is even."""
-    g = torch.Generator(device=device).manual_seed(seed)
-    pairs_target = (E - V) // 2
-    w = (torch.arange(V, device=device, dtype=torch.float64) + i0) ** (-alpha)
-    cdf = torch.cumsum(w, 0)
-    cdf /= cdf[-1].clone()
-    keys = torch.empty(0, dtype=torch.int64, device=device)
-    need = pairs_target
-    while keys.numel() < pairs_target:
-        m = int(need * 1.25) + 4096
-        a = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device, dtype=torch.float64))
-        b = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device, dtype=torch.float64))
-        a.clamp_(max=V - 1)
-        b.clamp_(max=V - 1)
-        lo, hi = torch.minimum(a, b), torch.maximum(a, b)
-        k = (lo * V + hi)[lo != hi]
-        keys = torch.unique(torch.cat([keys, k]))
-        need = pairs_target - keys.numel()
-        del a, b, lo, hi, k
-    keys = keys[torch.randperm(keys.numel(), generator=g, device=device)[:pairs_target]]
-    relabel = torch.randperm(V, generator=g, device=device)
-    lo, hi = relabel[keys // V], relabel[keys % V]
-    del keys
-    loops = torch.arange(V, device=device)
-    src = torch.cat([lo, hi, loops])
-    dst = torch.cat([hi, lo, loops])
-    del lo, hi
-    key = torch.sort(src * V + dst).values
-    del src, dst
-    src, dst = key // V, key % V
-    row_ptr = torch.zeros(V + 1, dtype=torch.int64, device=device)
-    row_ptr[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)
-    return row_ptr.to(torch.int32), dst.to(torch.int32)
 
 
 def alg_bytes(V, E, D, k, Vc=None):
@@ -206,7 +162,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--graph", default="reddit", choices=sorted(PRESETS))
+    ap.add_argument("--graph", default="reddit", choices=sorted(maxk_graph.PRESETS))
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
@@ -242,13 +198,12 @@ def main():
 
     import maxk_cuda_kernels as mk
 
-    P = dict(PRESETS[args.graph])
+    P = dict(maxk_graph.PRESETS[args.graph])
     D = args.dim or P["D"]
     k = args.k or P["k"]
     V = P["V"]
     E_target = P["E"] - ((P["E"] - V) % 2)
     t0 = time.time()
-    import maxk_graph
     gdir = maxk_graph.find_graph(args.graph, [args.graph_dir] if args.graph_dir else [])
     if gdir:
         g = maxk_graph.GraphDataLoader(gdir).load_graph(args.graph)
@@ -257,7 +212,7 @@ def main():
         V = g["v_num"]
         data = f"real graph {gdir}/{args.graph}.indptr|.indices; synthetic features"
     else:
-        row_ptr, col = make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
+        row_ptr, col = maxk_graph.make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
         data = "synthetic"
     E = col.numel()
     gen = torch.Generator(device=dev).manual_seed(123)  # kernels/main.cu:74-77 seed

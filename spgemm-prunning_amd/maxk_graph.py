@@ -12,6 +12,9 @@ sorts instead of a Python set loop, so the real Reddit / ogbn-products /
 ogbn-proteins graphs can be prepared on the GPU box in seconds; its output has
 sorted column indices, which the reference's DGL `adj_tensors('csr')` does not
 promise (the kernels accept either).
+
+`synthetic_graph` / `PRESETS`: the stand-ins used when the real files are absent
+(symmetric Chung-Lu power law with self loops at the published V and E).
 """
 from __future__ import annotations
 
@@ -128,3 +131,60 @@ def find_graph(name: str, dirs=None) -> Optional[str]:
                 os.path.exists(os.path.join(d, f"{name}.indices")):
             return d
     return None
+
+
+# ---------------------------------------------------------------------------- synthetic graphs
+# name: V, E (published sizes), power-law (alpha, offset) fitted so
+# the max/avg degree ratio resembles the real graph
+PRESETS = {
+    "reddit": dict(V=232_965, E=114_615_891, alpha=0.7, i0=200, D=256, k=16),
+    "products": dict(V=2_449_029, E=123_718_280, alpha=0.75, i0=3000, D=256, k=32),
+    "proteins": dict(V=132_534, E=79_122_504, alpha=0.45, i0=2000, D=256, k=64),
+    "flickr": dict(V=89_250, E=989_006, alpha=0.9, i0=30, D=64, k=16),
+}
+
+
+def make_graph(V, E, alpha, i0, seed, device):
+    """Symmetric Chung-Lu power-law graph with self loops, deduplicated, CSR with sorted
+    columns (the shape dataset_gen.py:44-115 produces), exactly E edges when E-V is even."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    pairs_target = (E - V) // 2
+    w = (torch.arange(V, device=device, dtype=torch.float64) + i0) ** (-alpha)
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    keys = torch.empty(0, dtype=torch.int64, device=device)
+    need = pairs_target
+    while keys.numel() < pairs_target:
+        m = int(need * 1.25) + 4096
+        a = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device, dtype=torch.float64))
+        b = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device, dtype=torch.float64))
+        a.clamp_(max=V - 1)
+        b.clamp_(max=V - 1)
+        lo, hi = torch.minimum(a, b), torch.maximum(a, b)
+        k = (lo * V + hi)[lo != hi]
+        keys = torch.unique(torch.cat([keys, k]))
+        need = pairs_target - keys.numel()
+        del a, b, lo, hi, k
+    keys = keys[torch.randperm(keys.numel(), generator=g, device=device)[:pairs_target]]
+    relabel = torch.randperm(V, generator=g, device=device)
+    lo, hi = relabel[keys // V], relabel[keys % V]
+    del keys
+    loops = torch.arange(V, device=device)
+    src = torch.cat([lo, hi, loops])
+    dst = torch.cat([hi, lo, loops])
+    del lo, hi
+    key = torch.sort(src * V + dst).values
+    del src, dst
+    src, dst = key // V, key % V
+    row_ptr = torch.zeros(V + 1, dtype=torch.int64, device=device)
+    row_ptr[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)
+    return row_ptr.to(torch.int32), dst.to(torch.int32)
+
+
+def synthetic_graph(name: str, seed: int = 1, device="cuda"):
+    """(row_ptr int32, col int32) of the synthetic stand-in for a published graph: its exact V,
+    E (E - V made even) and a degree skew like the real one."""
+    P = PRESETS[name]
+    V = P["V"]
+    E = P["E"] - ((P["E"] - V) % 2)
+    return make_graph(V, E, P["alpha"], P["i0"], seed, torch.device(device))

@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""maxk_kernel_test -- the reference's kernel benchmark, on MI355X.
+
+Restates `./maxk_kernel_test <graph>` (kernels/main.cu:50-221): for each k of
+{16, 32, 64} (main.cu:111-117) every row gets k distinct columns of D sampled uniformly,
+in ascending order, with U(0,1) values (main.cu:122-133); the dense copy of that input is
+multiplied by the sparse library SpMM (rocSPARSE here, cuSPARSE there, main.cu:163-166)
+once, then the MaxK forward SpGEMM and backward SSpMM are timed (spmm_base.h:34-61).
+Output keeps the reference's lines:
+
+    num graph dim_origin dim_k kernel time(ms)
+    1/1 reddit 256 16 cusparse 20.1
+    1/1 reddit 256 16 maxk 1.70
+    1/1 reddit 256 16 maxk_backward 4.70
+
+Graph: <dir>/<graph>.indptr|.indices when present (maxk_graph.find_graph: MAXK_GRAPH_DIR,
+kernels/graphs, processed_graphs, graphs), else the synthetic stand-in of the same size.
+Timing: HIP events on the current stream, median of --runs after --warmup (the reference
+used 4 + 4 wall-clock runs).  Adds one validation line per k: MaxK forward vs the library
+SpMM, max |diff| / max(1, |ref|) (the reference's check: direct_kernel_interface.py:221-372).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import maxk_cuda_kernels as mk  # noqa: E402
+import maxk_graph  # noqa: E402
+
+
+def sample_cbsr(V: int, D: int, k: int, gen: torch.Generator, device):
+    """main.cu:122-133: k distinct columns per row (ascending) with U(0,1) values."""
+    keys = torch.rand(V, D, generator=gen, device=device)
+    sel = torch.topk(keys, k, dim=1).indices.sort(dim=1).values.to(torch.uint8).contiguous()
+    vals = torch.rand(V, k, generator=gen, device=device)
+    return vals, sel
+
+
+def time_ms(fn, warmup: int, runs: int) -> float:
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(runs):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("graph", nargs="?", default="reddit")
+    ap.add_argument("--k", type=int, nargs="+", default=[16, 32, 64])
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--graph-dir", default=None)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--runs", type=int, default=20)
+    ap.add_argument("--bwd-mode", default="csc", choices=["csc", "atomic"])
+    ap.add_argument("--json", action="store_true", help="also print one JSON summary line")
+    args = ap.parse_args(argv)
+    if not torch.cuda.is_available():
+        raise SystemExit("maxk_kernel_test needs an MI355X (HIP device)")
+    dev = torch.device("cuda")
+    gdir = maxk_graph.find_graph(args.graph, [args.graph_dir] if args.graph_dir else [])
+    if gdir:
+        g = maxk_graph.GraphDataLoader(gdir).load_graph(args.graph)
+        row_ptr = torch.from_numpy(g["indptr"]).to(dev)
+        col = torch.from_numpy(g["indices"]).to(dev)
+        source = f"{gdir}/{args.graph}.indptr|.indices"
+    elif args.graph in maxk_graph.PRESETS:
+        row_ptr, col = maxk_graph.synthetic_graph(args.graph, device=dev)
+        source = "synthetic"
+    else:
+        raise SystemExit(f"no {args.graph}.indptr/.indices found and no synthetic preset "
+                         f"(presets: {sorted(maxk_graph.PRESETS)})")
+    V, E, D = row_ptr.numel() - 1, col.numel(), args.dim
+    gen = torch.Generator(device=dev).manual_seed(123)  # main.cu:74-77
+    val = torch.rand(E, generator=gen, device=dev)
+    plan = mk.transpose_plan(col, V) if args.bwd_mode == "csc" else None
+    print(f"# graph {args.graph} ({source}): V={V} E={E}", file=sys.stderr)
+    print("num graph dim_origin dim_k kernel time(ms)")
+    results = []
+    t_lib = None
+    for n, k in enumerate(args.k):
+        tag = f"1/1 {args.graph} {D} {k}"
+        vals, sel = sample_cbsr(V, D, k, gen, dev)
+        dense = mk.cbsr_scatter_dense(vals, sel, D)
+        y = torch.empty(V, D, device=dev)
+        gs = torch.empty(V, k, device=dev)
+        mk.spgemm_forward(row_ptr, col, val, vals, sel, D, out=y, validate=True)
+        if n == 0:  # main.cu:163-166: the library SpMM once, on the first k's dense input
+            lib = mk.DenseSpMMPlan(row_ptr, col, val, dense)
+            t_lib = time_ms(lib.run, args.warmup, args.runs)
+            print(f"{tag} cusparse {t_lib:.4f}")
+        else:
+            lib = mk.DenseSpMMPlan(row_ptr, col, val, dense)
+            lib.run()
+        torch.cuda.synchronize()
+        err = float(((y - lib.y).abs().max() / lib.y.abs().max().clamp(min=1)))
+        lib.close()
+        t_f = time_ms(lambda: mk.spgemm_forward(row_ptr, col, val, vals, sel, D, out=y,
+                                                validate=False), args.warmup, args.runs)
+        print(f"{tag} maxk {t_f:.4f}")
+        t_b = time_ms(lambda: mk.sspmm_backward(row_ptr, col, val, dense, sel, out=gs,
+                                                validate=False, mode=args.bwd_mode, plan=plan),
+                      args.warmup, args.runs)
+        print(f"{tag} maxk_backward {t_b:.4f}")
+        print(f"# {tag} check maxk vs library SpMM: max rel err {err:.3e} "
+              f"({'PASS' if err < 1e-3 else 'FAIL'})", file=sys.stderr)
+        results.append({"k": k, "maxk_ms": t_f, "maxk_backward_ms": t_b, "max_rel_err": err,
+                        "speedup_fwd": t_lib / t_f, "speedup_bwd": t_lib / t_b,
+                        "gteps_fwd": E / t_f / 1e6, "gteps_bwd": E / t_b / 1e6})
+        del dense, y, gs
+    if args.json:
+        print(json.dumps({"graph": args.graph, "source": source, "V": V, "E": E, "dim": D,
+                          "library_spmm_ms": t_lib, "bwd_mode": args.bwd_mode,
+                          "results": results}))
+    return results
+
+
+if __name__ == "__main__":
+    main()

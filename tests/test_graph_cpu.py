@@ -94,3 +94,33 @@ def test_build_csr_on_device_matches_cpu(cuda):
     a = mg.build_csr(torch.from_numpy(src), torch.from_numpy(dst), 5000)
     b = mg.build_csr(torch.from_numpy(src).to(cuda), torch.from_numpy(dst).to(cuda), 5000)
     assert torch.equal(a[0], b[0].cpu()) and torch.equal(a[1], b[1].cpu())
+
+
+def test_synthetic_generator_properties():
+    """make_graph (bench / maxk_kernel_test stand-ins): exact E, symmetric, self loop on every
+    vertex, no duplicates, sorted columns."""
+    V, E = 3000, 3000 + 2 * 25000
+    ip, ix = mg.make_graph(V, E, 0.7, 30, 1, torch.device("cpu"))
+    assert ip.dtype == torch.int32 and ix.dtype == torch.int32 and ix.numel() == E
+    edges = set(_csr_edges(ip, ix))
+    assert len(edges) == E
+    assert all((d, s) in edges for s, d in edges)
+    assert all((v, v) in edges for v in range(V))
+    ipn, ixn = ip.numpy(), ix.numpy()
+    assert all((np.diff(ixn[ipn[r]:ipn[r + 1]]) > 0).all() for r in range(V))
+    deg = np.diff(ipn)
+    assert deg.max() > 5 * deg.mean()  # power-law skew
+    ip2, ix2 = mg.make_graph(V, E, 0.7, 30, 1, torch.device("cpu"))
+    assert torch.equal(ip, ip2) and torch.equal(ix, ix2)  # seeded
+
+
+@pytest.mark.gpu
+def test_kernel_test_cli(cuda, capsys):
+    import maxk_kernel_test
+    res = maxk_kernel_test.main(["flickr", "--k", "16", "32", "--dim", "64", "--warmup", "1",
+                                 "--runs", "3", "--json"])
+    out = capsys.readouterr().out.splitlines()
+    assert out[0] == "num graph dim_origin dim_k kernel time(ms)"
+    assert out[1].startswith("1/1 flickr 64 16 cusparse ")
+    assert [r["k"] for r in res] == [16, 32]
+    assert all(r["max_rel_err"] < 1e-3 and r["maxk_ms"] > 0 for r in res)

@@ -201,6 +201,24 @@ def test_all_k_against_oracle(mk, cuda, k, D):
     assert np.array_equal(i.cpu().numpy(), ci) and np.array_equal(v.cpu().numpy(), cv)
 
 
+@pytest.mark.parametrize("k", [16, 12, 10, 64])
+def test_high_degree_against_oracle(mk, cuda, k):
+    """Average degree ~500 (Reddit-like): the backward picks its deepest batches (phase 1
+    U=16, phase 2 U=8); k=16/64 take the float4 phase 2, 12 the padded 4-l-per-lane phase 1,
+    10 the one-l-per-lane path."""
+    rng = np.random.default_rng(77 + k)
+    V, D = 2000, 256
+    row_ptr, col = rand_graph(rng, V, 500, hubs=((7, 1999),))
+    val = rng.random(col.size, dtype=np.float32)
+    x = rng.standard_normal((V, D), dtype=np.float32)
+    cv, ci = O.topk(x, k)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+    y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, 0, "csc")
+    close(y, yo)
+    close(gs, go)
+
+
 def test_empty_graph_and_empty_rows(mk, cuda):
     D, k, V = 64, 16, 50
     rng = np.random.default_rng(1)
