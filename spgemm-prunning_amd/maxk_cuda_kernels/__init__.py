@@ -57,8 +57,44 @@ def device_count() -> int:
     return _lib().maxk_device_count()
 
 
+def _validate_mode() -> str:
+    """MAXK_VALIDATE: unset -> check each graph once (cached per tensor, like the transpose
+    plan); "1" -> check every call (graph and selectors); "0" -> never check."""
+    v = os.environ.get("MAXK_VALIDATE", "")
+    return "once" if v == "" else ("never" if v == "0" else "always")
+
+
 def _validate_default() -> bool:
-    return os.environ.get("MAXK_VALIDATE", "0") not in ("", "0")
+    return _validate_mode() == "always"
+
+
+_CHECKED: "dict" = {}
+
+
+def _check_graph_once(row_ptr, col_idx, num_cols):
+    """Out-of-range row_ptr / col_idx are the only inputs that can make a kernel read out of
+    bounds (a u8 selector always indexes inside a 256-entry row), so each graph is validated
+    the first time it is used; the check is cached on the tensors' identity and versions."""
+    key = (id(row_ptr), id(col_idx))
+    hit = _CHECKED.get(key)
+    if hit is not None:
+        rr, cr, rv, cv, nc = hit
+        if rr() is row_ptr and cr() is col_idx and rv == row_ptr._version and \
+                cv == col_idx._version and nc == num_cols:
+            return
+    _validate_graph(row_ptr, col_idx, num_cols, col_idx.numel())
+    if key not in _CHECKED:
+        weakref.finalize(col_idx, _CHECKED.pop, key, None)
+    _CHECKED[key] = (weakref.ref(row_ptr), weakref.ref(col_idx), row_ptr._version,
+                     col_idx._version, int(num_cols))
+
+
+def _validate_call(validate, row_ptr, col_idx, num_cols, sel, D):
+    if validate if validate is not None else _validate_default():
+        _validate_graph(row_ptr, col_idx, num_cols, col_idx.numel())
+        _validate_selector(sel, D)
+    elif validate is None and _validate_mode() == "once":
+        _check_graph_once(row_ptr, col_idx, num_cols)
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -174,9 +210,7 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         _need(row_div, "row_div", torch.float32)
         if row_div.numel() != num_rows:
             raise RuntimeError("row_div must have num_rows entries")
-    if validate if validate is not None else _validate_default():
-        _validate_graph(indptr, indices, num_cols, indices.numel())
-        _validate_selector(cbsr_idx, D)
+    _validate_call(validate, indptr, indices, num_cols, cbsr_idx, D)
     dev = cbsr_val.device
     if out is None:
         out = torch.empty(num_rows, D, dtype=torch.float32, device=dev)
@@ -259,9 +293,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         _need(row_div, "row_div", torch.float32)
         if row_div.numel() != num_rows:
             raise RuntimeError("row_div must have num_rows entries")
-    if validate if validate is not None else _validate_default():
-        _validate_graph(indptr, indices, num_cols, indices.numel())
-        _validate_selector(cbsr_idx, D)
+    _validate_call(validate, indptr, indices, num_cols, cbsr_idx, D)
     dev = grad_output.device
     if out is None:
         out = torch.empty(num_cols, k, dtype=torch.float32, device=dev)

@@ -76,11 +76,11 @@ class _HipKernels:
 
     def spgemm_forward(self, indptr, indices, values, cbsr_val, cbsr_idx, D, row_div=None):
         return self.mk.spgemm_forward(indptr, indices, values, cbsr_val, cbsr_idx, D,
-                                      row_div=row_div, validate=False)
+                                      row_div=row_div)
 
     def sspmm_backward(self, indptr, indices, values, grad, cbsr_idx, row_div=None, plan=None):
         return self.mk.sspmm_backward(indptr, indices, values, grad, cbsr_idx, row_div=row_div,
-                                      validate=False, plan=plan)
+                                      plan=plan)
 
     def transpose_plan(self, indices, num_cols):
         return self.mk.transpose_plan(indices, num_cols)

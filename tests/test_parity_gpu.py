@@ -381,3 +381,27 @@ def test_adjoint_identity_large(mk, cuda):
     # row sums: sum_j Y[r, j] == A . (sum_l v[c, l])
     rs = torch.sparse_csr_tensor(row_ptr.long(), dst.long(), val, (V, V)) @ v.sum(1, keepdim=True)
     assert torch.allclose(y.sum(1), rs[:, 0], rtol=1e-4, atol=1e-3)
+
+
+def test_graph_checked_once_by_default(mk, cuda, monkeypatch):
+    """MAXK_VALIDATE unset: a bad graph is refused on first use (no out-of-bounds launch); a
+    checked graph is not re-checked until one of its tensors is modified in place."""
+    monkeypatch.setenv("MAXK_VALIDATE", "")
+    rng = np.random.default_rng(5)
+    row_ptr, col = rand_graph(rng, 300, 8)
+    val = rng.random(col.size, dtype=np.float32)
+    cv, ci = O.topk(rng.standard_normal((300, 64), dtype=np.float32), 8)
+    rp, cl, vl, cvt, cit = (T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda),
+                            T(ci, cuda))
+    y = mk.spgemm_forward(rp, cl, vl, cvt, cit, 64)
+    close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, 64))
+    cl[5] = 300  # out of range, in place: the version bump forces a new check
+    with pytest.raises(RuntimeError, match="col_idx out of range"):
+        mk.spgemm_forward(rp, cl, vl, cvt, cit, 64)
+    with pytest.raises(RuntimeError, match="col_idx out of range"):
+        mk.sspmm_backward(rp, cl, vl, T(rng.standard_normal((300, 64), dtype=np.float32), cuda),
+                          cit)
+    bad_rp = rp.clone()
+    bad_rp[-1] += 1
+    with pytest.raises(RuntimeError, match="row_ptr"):
+        mk.spgemm_forward(bad_rp, T(col, cuda), vl, cvt, cit, 64)
