@@ -33,9 +33,6 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #ifndef MAXK_XCD_SUM  // XCD-contiguous work order in the backward's phase 2
 #define MAXK_XCD_SUM 1
 #endif
-#ifndef MAXK_XCD_FWD  // ... and in the forward
-#define MAXK_XCD_FWD 0
-#endif
 #ifndef MAXK_BWD_X4  // 4-l-per-lane phase 1 of the two-phase backward (k % 4 == 0)
 #define MAXK_BWD_X4 1
 #endif
@@ -45,20 +42,8 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif
-#ifndef MAXK_NT_STREAM  // non-temporal loads of the single-use CSR streams (col_idx, val, eid)
-#define MAXK_NT_STREAM 0
-#endif
-#ifndef MAXK_NT_TLOAD  // non-temporal loads of the contribution rows in phase 2
-#define MAXK_NT_TLOAD 0
-#endif
-#ifndef MAXK_TOPK_RADIX  // top-k threshold by 8-bit radix select (else bit construction)
-#define MAXK_TOPK_RADIX 1
-#endif
 #ifndef MAXK_TOPK_BLOCKS  // grid cap of the grid-stride top-k (rows per wave grow past it)
 #define MAXK_TOPK_BLOCKS 16384
-#endif
-#ifndef MAXK_BWD_ROWWIN  // phase 1: row_ptr/row_div window in registers + next-row G prefetch
-#define MAXK_BWD_ROWWIN 1
 #endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
@@ -113,32 +98,6 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // grid = 8 * per, logical block (b % 8) * per + b / 8 makes XCD x run the contiguous
 // logical range [x * per, (x + 1) * per) in launch order, so work items that are
 // neighbours (and touch neighbouring lines) share one L2 instead of eight.
-template <typename V>
-__device__ __forceinline__ V ld_stream(const V *p) {
-#if MAXK_NT_STREAM
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-template <typename V>
-__device__ __forceinline__ V ld_trow(const V *p) {
-#if MAXK_NT_TLOAD
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ float4 ld_trow(const float4 *p) {
-#if MAXK_NT_TLOAD
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-
 constexpr int kXcds = 8;
 inline int64_t xcd_grid(int64_t blocks) { return (blocks + kXcds - 1) / kXcds * kXcds; }
 __device__ __forceinline__ int xcd_contiguous_block(int b, int grid) {

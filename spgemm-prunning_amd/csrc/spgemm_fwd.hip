@@ -107,8 +107,8 @@ struct EdgeWalker {
             for (int u = 0; u < U; ++u) {
                 const int e = base + u * G + grp;
                 const int ec = e < se ? e : last;
-                c[u] = ld_stream(col_idx + ec);
-                const float wv = ld_stream(edge_val + ec);
+                c[u] = col_idx[ec];
+                const float wv = edge_val[ec];
                 w[u] = e < se ? wv : 0.f;
             }
             for (int lb = 0; lb < k; lb += KG) {  // one pass unless k > 64
@@ -182,8 +182,7 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int blk = MAXK_XCD_FWD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int item = blk * kWavesPerBlock + wid;
+    const int item = blockIdx.x * kWavesPerBlock + wid;
     if (item >= n_items) return;  // whole wave; no workgroup barrier below
     float *acc = lds + (size_t)wid * NC * DS;
     for (int j = lane * 4; j < NC * DS; j += kWave * 4)
@@ -289,8 +288,7 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
     constexpr int U = MAXK_FWD_U;
     constexpr int NC = kWave / KG;
     const size_t lds = (size_t)kWavesPerBlock * NC * L.DS * sizeof(float);
-    const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
-    const dim3 grid((unsigned)(MAXK_XCD_FWD ? xcd_grid(blocks) : blocks));
+    const dim3 grid((unsigned)ceil_div(L.n_items, kWavesPerBlock));
     hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U>), grid, dim3(kBlock), lds, s, row_ptr, col_idx,
                        edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows, num_e, D,
                        L.DS, k, L.chunk, L.n_items);

@@ -4,22 +4,22 @@
 // Semantics: kernels/spmm_maxk_backward.cu:15-115 (push from the CSR of A, which
 // yields the A^T product) and the /out_degrees of maxk_spgemm_function.py:154-155.
 //
-// The push reads every G row once (staged in LDS, 16-B loads) and produces one
-// k-float contribution per edge that must be summed per destination c.  Two
-// forms of that sum:
+// The push reads every G row once (staged in LDS) and produces one k-float
+// contribution per edge that must be summed per destination c.  Two forms of
+// that sum:
 //  * atomic (maxk_sspmm_backward): one global fp32 atomic per (edge, l) into
-//    grad_cbsr (zeroed first).  No preprocessing, but E*k*4 bytes of memory-side
-//    atomics, which MI355X executes at ~1.3 TB/s chip-wide
-//    (MI355X_MICROARCH.md, Global float atomics) -- the kernel sits exactly on
-//    that ceiling (6.2 ms for Reddit-sized k=16).
-//  * two-phase (maxk_sspmm_backward_csc, needs maxk_transpose_plan): phase 1
-//    stores each edge's contribution row in CSR edge order (streaming stores;
-//    scattering them to CSC slots instead measured 4.7 ms, partial-line writes);
-//    phase 2 gathers the rows of each destination through the CSC permutation
-//    and sums them in a fixed order (cross-lane butterflies).  2*E*k*4 bytes of
-//    plain traffic instead of E*k*4 of atomics, and bitwise deterministic.
+//    grad_cbsr (zeroed first).  MI355X executes float atomics memory-side and
+//    they are bound by request count: ~6 ms for Reddit-sized at any k in 2..16.
+//  * two-phase (maxk_sspmm_backward_csc, default, needs maxk_transpose_plan):
+//    phase 1 stores each edge's contribution row in CSR edge order (non-temporal
+//    16-B buffer stores, so the 7.3 GB stream does not evict the selector table
+//    every edge gathers from); phase 2 gathers the rows of each destination
+//    through the CSC permutation and sums them in a fixed order.  Bitwise
+//    deterministic; per edge one L2-resident selector lookup plus one random
+//    64-B row read, which is the floor this structure can reach.
 // Both use the token-stream work partition of common.h (one wave per item of C
-// tokens, hub rows split, short rows batched).
+// tokens, hub rows split, short rows batched); loads-in-flight depth per launch
+// from the average degree (pick_depth).
 #include "common.h"
 
 namespace maxk {
@@ -64,8 +64,8 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
     for (int u = 0; u < U; ++u) {
         const int e = sb + u * G + grp;
         const int ec = e < se ? e : last;
-        c[u] = ld_stream(col_idx + ec);
-        w[u] = ld_stream(edge_val + ec);
+        c[u] = col_idx[ec];
+        w[u] = edge_val[ec];
     }
     u32x4 xp[U];
     uint32_t op[U];
@@ -79,8 +79,8 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
             for (int u = 0; u < U; ++u) {
                 const int e = base + GU + u * G + grp;
                 const int ec = e < se ? e : last;
-                cn[u] = ld_stream(col_idx + ec);
-                wn[u] = ld_stream(edge_val + ec);
+                cn[u] = col_idx[ec];
+                wn[u] = edge_val[ec];
             }
         }
         uint32_t sv[U];
@@ -146,8 +146,8 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
     for (int u = 0; u < U; ++u) {
         const int e = sb + u * G + grp;
         const int ec = e < se ? e : last;
-        c[u] = ld_stream(col_idx + ec);
-        w[u] = ld_stream(edge_val + ec);
+        c[u] = col_idx[ec];
+        w[u] = edge_val[ec];
     }
     if (MODE == kStore && k <= KG) {
         const bool lok = l0 < k;
@@ -164,33 +164,23 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
                 for (int u = 0; u < U; ++u) {
                     const int e = base + GU + u * G + grp;
                     const int ec = e < se ? e : last;
-                    cn[u] = ld_stream(col_idx + ec);
-                    wn[u] = ld_stream(edge_val + ec);
+                    cn[u] = col_idx[ec];
+                    wn[u] = edge_val[ec];
                 }
             }
             int s[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-#ifdef MAXK_ABLATE_NOSEL
-                s[u] = (c[u] + lc * 16) & 255;
-#else
                 s[u] = cbsr_idx[c[u] * k + lc];
-#endif
             }
-#ifndef MAXK_ABLATE_NOSTORE
             if (pending) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) dst[(size_t)(uint32_t)rp[u] * k + lc] = xp[u];
             }
-#endif
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int e = base + u * G + grp;
-#ifdef MAXK_ABLATE_NOSTORE
-                xp[u] += w[u] * g_lds[s[u]];
-#else
                 xp[u] = w[u] * g_lds[s[u]];
-#endif
                 rp[u] = (e < se && lok) ? e : dummy;
             }
             pending = true;
@@ -230,31 +220,10 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
         for (int u = 0; u < U; ++u) {
             const int e = base + GU + u * G + grp;
             const int ec = e < se ? e : last;
-            c[u] = ld_stream(col_idx + ec);
-            w[u] = ld_stream(edge_val + ec);
+            c[u] = col_idx[ec];
+            w[u] = edge_val[ec];
         }
     }
-}
-
-// g_lds[0:D] = grad[0:D] / div   (one wave; g_lds[D:256] stays 0)
-__device__ __forceinline__ void stage_row(float *g_lds, const float *__restrict__ grad, int D,
-                                          float div, bool scale, int lane) {
-    wave_lds_fence();
-    if ((D & 3) == 0) {
-        for (int j = lane * 4; j < D; j += kWave * 4) {
-            float4 a = *reinterpret_cast<const float4 *>(&grad[j]);
-            if (scale) {
-                a.x = a.x / div;
-                a.y = a.y / div;
-                a.z = a.z / div;
-                a.w = a.w / div;
-            }
-            *reinterpret_cast<float4 *>(&g_lds[j]) = a;
-        }
-    } else {
-        for (int j = lane; j < D; j += kWave) g_lds[j] = scale ? grad[j] / div : grad[j];
-    }
-    wave_lds_fence();
 }
 
 template <int KG, int U, int MODE>
@@ -275,7 +244,6 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
     const int64_t d0 = (int64_t)item * chunk;
     const int64_t d1 = d0 + chunk < total ? d0 + chunk : total;
     int r = wave_first_row_token(row_ptr, num_rows, d0);
-#if MAXK_BWD_ROWWIN
     // Rows q = r-1 (continuation), r, r+1, ...: the item's edges of row q are
     // [max(rb, d0-q-1), min(re, d1-q-1)).  row_ptr / row_div of 64 consecutive rows sit
     // one per lane (read with readlane), and each row's G values (4 per lane, columns
@@ -323,30 +291,6 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
         push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)sb64,
                                 (int)se64, k, lane);
     }
-#else
-    if (r > 0) {  // continuation of row r-1
-        const int64_t sb = d0 - r;
-        int64_t se = (int64_t)row_ptr[r];
-        if (d1 - r < se) se = d1 - r;
-        if (sb < se) {
-            const float div = row_div ? row_div[r - 1] : 1.f;
-            stage_row(g_lds, grad + (int64_t)(r - 1) * D, D, div, row_div != nullptr, lane);
-            push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)sb,
-                                    (int)se, k, lane);
-        }
-    }
-    for (; r < num_rows; ++r) {
-        const int64_t rb = row_ptr[r];
-        if (rb + r >= d1) break;
-        int64_t se = (int64_t)row_ptr[r + 1];
-        if (d1 - r - 1 < se) se = d1 - r - 1;
-        if (rb >= se) continue;  // empty row: nothing to push
-        const float div = row_div ? row_div[r] : 1.f;
-        stage_row(g_lds, grad + (int64_t)r * D, D, div, row_div != nullptr, lane);
-        push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)rb,
-                                (int)se, k, lane);
-    }
-#endif
 }
 
 // ---- phase 2: grad_cbsr[c, :] = sum over the CSC slots t of c of T[eid[t], :] -------
@@ -369,8 +313,8 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t t = base + u * RI + g;
-                const int e = ld_stream(eid + (t < te ? t : tb));
-                v[u] = ld_trow(T4 + (size_t)(uint32_t)e * LR + q);
+                const int e = eid[t < te ? t : tb];
+                v[u] = T4[(size_t)(uint32_t)e * LR + q];
                 if (t >= te) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
@@ -400,8 +344,8 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int64_t t = base + u * G + grp;
-                    const int e = ld_stream(eid + (t < te ? t : tb));
-                    v[u] = ld_trow(T + (size_t)(uint32_t)e * k + lc);
+                    const int e = eid[t < te ? t : tb];
+                    v[u] = T[(size_t)(uint32_t)e * k + lc];
                     if (t >= te) v[u] = 0.f;
                 }
 #pragma unroll

@@ -10,8 +10,8 @@
 //  1. order-preserving 32-bit keys (NaN above +inf, as torch ranks it);
 //  2. the k-th largest key T by MSB-first radix select over 8-bit digits
 //     (per-wave 256-bin LDS histogram + wave suffix scan; 4 passes for f32).
-//     The earlier bit-by-bit construction (32 dependent ballot/popcount
-//     rounds, MAXK_TOPK_RADIX=0) was bound by the CU's shared scalar unit;
+//     (An earlier bit-by-bit construction, 32 dependent ballot/popcount rounds,
+//     was bound by the CU's single scalar unit.)
 //  3. select key > T, plus the lowest-column key == T until k are taken;
 //  4. compact the k winners into LDS, rank each against the others
 //     (broadcast LDS reads) and store in (key desc, column asc) order.
@@ -48,9 +48,7 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
     __shared__ __attribute__((aligned(16))) uint32_t s_key[kWavesPerBlock][kSlots];
     __shared__ T s_val[kWavesPerBlock][kSlots];
     __shared__ __attribute__((aligned(16))) uint8_t s_col[kWavesPerBlock][kSlots];
-#if MAXK_TOPK_RADIX
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[kWavesPerBlock][256];
-#endif
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
     const uint64_t lt_mask = (1ull << lane) - 1ull;
@@ -87,7 +85,6 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
     }
 
     // T = max t such that #{key >= t} >= k  (the k-th largest key)
-#if MAXK_TOPK_RADIX
     // MSB-first radix select, 8-bit digits: per pass a 256-bin histogram of the keys
     // still matching the chosen prefix (integer LDS atomics), a wave suffix scan of the
     // bins, and the largest digit whose suffix count still reaches `need`.
@@ -95,11 +92,7 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
     int need = k;  // how many of the keys matching the prefix are still to be taken
     int sh = 0;    // selection compares key >> sh with thr >> sh (sh > 0 after an early exit)
     uint32_t *hist = s_hist[wid];
-#if MAXK_TOPK_ABLATE & 2
-    for (int shift = -8; shift >= 0; shift -= 8) {
-#else
     for (int shift = KeyBits<T>::value - 8; shift >= 0; shift -= 8) {
-#endif
         reinterpret_cast<uint4 *>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_fence();
 #pragma unroll
@@ -137,21 +130,6 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
     }
     const int need_eq = need;
     thr >>= sh;
-#else
-    const int sh = 0;
-    uint32_t thr = 0;
-    for (int bit = KeyBits<T>::value - 1; bit >= 0; --bit) {
-        const uint32_t cand = thr | (1u << bit);
-        int cnt = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) cnt += __popcll(__ballot(ok[i] && key[i] >= cand));
-        if (cnt >= k) thr = cand;
-    }
-    int n_gt = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) n_gt += __popcll(__ballot(ok[i] && key[i] > thr));
-    const int need_eq = k - n_gt;
-#endif
 
     // select, then compact winners into LDS slots [0, k)
     const int k4 = (k + 3) & ~3;
@@ -180,9 +158,6 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
         const uint32_t kp = s_key[wid][p];
         const int cp = s_col[wid][p];
         int pos = 0;
-#if MAXK_TOPK_ABLATE & 1
-        pos = p;
-#else
         for (int q = 0; q < k4; q += 4) {
             const uint4 kq = *reinterpret_cast<const uint4 *>(&s_key[wid][q]);
             const uint32_t cq = *reinterpret_cast<const uint32_t *>(&s_col[wid][q]);
@@ -191,7 +166,6 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
             pos += (kq.z > kp) || (kq.z == kp && (int)((cq >> 16) & 255u) < cp);
             pos += (kq.w > kp) || (kq.w == kp && (int)(cq >> 24) < cp);
         }
-#endif
         const int64_t o = (int64_t)row * k + pos;
         out_val[o] = s_val[wid][p];
         out_idx[o] = (uint8_t)cp;
