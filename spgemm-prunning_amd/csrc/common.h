@@ -45,6 +45,12 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #ifndef MAXK_TOPK_BLOCKS  // grid cap of the grid-stride top-k (rows per wave grow past it)
 #define MAXK_TOPK_BLOCKS 16384
 #endif
+#ifndef MAXK_P1_ITEMS  // backward auto item size: items per resident wave slot (phase 1 / 2)
+#define MAXK_P1_ITEMS 16
+#endif
+#ifndef MAXK_P2_ITEMS
+#define MAXK_P2_ITEMS 16
+#endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
 #endif

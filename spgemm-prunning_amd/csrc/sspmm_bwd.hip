@@ -414,10 +414,11 @@ __global__ __launch_bounds__(kBlock) void csc_sum_fixup_kernel(const float *__re
     }
 }
 
-int bwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk) {
+// Auto item size: ~`per_slot` items per resident wave slot on 256 CUs, in [256, 2048].
+int bwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int per_slot) {
     if (chunk > 0) return chunk;
     const int64_t total = num_rows + num_e;
-    int64_t c = ceil_div(total, 256LL * 32 * 8);
+    int64_t c = ceil_div(total, 256LL * 32 * per_slot);
     c = c < 256 ? 256 : (c > 2048 ? 2048 : c);
     return (int)c;
 }
@@ -512,7 +513,7 @@ struct CscLayout {
 
 CscLayout csc_layout(int64_t num_cols, int64_t num_e, int k, int chunk) {
     CscLayout L{};
-    L.chunk = bwd_chunk(num_cols, num_e, chunk);
+    L.chunk = bwd_chunk(num_cols, num_e, chunk, MAXK_P2_ITEMS);
     L.n_items = n_items_for(num_cols, num_e, L.chunk);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     L.t_bytes = al((size_t)(num_e + 1) * k * sizeof(float));  // + dummy row for masked lanes
@@ -568,7 +569,7 @@ extern "C" int maxk_sspmm_backward(const int32_t *row_ptr, const int32_t *col_id
     MAXK_REQUIRE(num_cols > 0, "edges present but num_cols == 0");
     return launch_push<kAtomic>(s, row_ptr, col_idx, edge_val, grad_out, row_div, cbsr_idx,
                                 grad_cbsr, (int)num_rows, num_e, dim_origin, dim_k,
-                                bwd_chunk(num_rows, num_e, chunk_edges));
+                                bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS));
 }
 
 extern "C" size_t maxk_sspmm_backward_csc_workspace_size(int64_t num_rows, int64_t num_cols,
@@ -606,12 +607,11 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
     if (num_e > 0 && num_rows > 0) {
         if (int rc = launch_push<kStore>(s, row_ptr, col_idx, edge_val, grad_out, row_div,
                                          cbsr_idx, T, (int)num_rows, num_e, dim_origin,
-                                         k, bwd_chunk(num_rows, num_e, chunk_edges)))
+                                         k, bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS)))
             return rc;
     }
     const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
     const dim3 grid((unsigned)(MAXK_XCD_SUM ? xcd_grid(blocks) : blocks));
-    const dim3 fix_grid((unsigned)blocks);
     const int nc = (int)num_cols;
     if (vec_sum(k)) {
         const int rows_per_step = kWave / (k / 4);
@@ -649,8 +649,8 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
         }
     }
     MAXK_LAUNCHED("csc_sum_kernel");
-    hipLaunchKernelGGL(csc_sum_fixup_kernel, fix_grid, dim3(kBlock), 0, s, slab, slab_row, grad_cbsr,
-                       k, L.n_items);
+    hipLaunchKernelGGL(csc_sum_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, slab,
+                       slab_row, grad_cbsr, k, L.n_items);
     MAXK_LAUNCHED("csc_sum_fixup_kernel");
     return MAXK_OK;
 }
