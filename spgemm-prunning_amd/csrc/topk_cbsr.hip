@@ -8,8 +8,10 @@
 // One wavefront per row (D <= 256, so <= 4 elements per lane, column
 // j = lane + 64*i for coalesced loads):
 //  1. order-preserving 32-bit keys (NaN above +inf, as torch ranks it);
-//  2. the k-th largest key T by MSB-first radix select over 8-bit digits
-//     (per-wave 256-bin LDS histogram + wave suffix scan; 4 passes for f32).
+//  2. the k-th largest key T by MSB-first radix select over data-adaptive
+//     8-bit digits (wave min/max of the keys in play, then a per-wave 256-bin
+//     LDS histogram of the 8 bits below their common prefix + a wave suffix scan;
+//     usually one pass).
 //     (An earlier bit-by-bit construction, 32 dependent ballot/popcount rounds,
 //     was bound by the CU's single scalar unit.)
 //  3. select key > T, plus the lowest-column key == T until k are taken;
@@ -27,14 +29,6 @@ __device__ __forceinline__ uint32_t order_key(float x) {
 }
 __device__ __forceinline__ uint32_t order_key(uint8_t x) { return x; }
 
-template <typename T>
-struct KeyBits {
-    static constexpr int value = 32;
-};
-template <>
-struct KeyBits<uint8_t> {
-    static constexpr int value = 8;
-};
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__ x, int64_t ld_x,
@@ -84,19 +78,44 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
         for (int i = 0; i < 4; ++i) vn[i] = xr[col4[i]];
     }
 
-    // T = max t such that #{key >= t} >= k  (the k-th largest key)
-    // MSB-first radix select, 8-bit digits: per pass a 256-bin histogram of the keys
-    // still matching the chosen prefix (integer LDS atomics), a wave suffix scan of the
-    // bins, and the largest digit whose suffix count still reaches `need`.
+    // T = max t such that #{key >= t} >= k  (the k-th largest key), by MSB-first radix
+    // select with data-adaptive 8-bit digits: each pass takes the wave min / max of the
+    // keys still in play and histograms the 8 bits right below their common prefix
+    // (256-bin LDS histogram, integer atomics), then keeps the largest digit whose suffix
+    // count still reaches `need`.  Real activations share their top bits (sign, exponent),
+    // so a fixed top-byte digit would pile them into one bin; the adaptive digit spreads
+    // them, and the pass usually ends the search (the chosen bin holds exactly the keys
+    // still needed).
     uint32_t thr = 0, pmask = 0;
-    int need = k;  // how many of the keys matching the prefix are still to be taken
-    int sh = 0;    // selection compares key >> sh with thr >> sh (sh > 0 after an early exit)
+    int need = k;  // how many of the keys in play are still to be taken
+    int sh = 0;    // selection compares key >> sh with thr (after the final shift)
     uint32_t *hist = s_hist[wid];
-    for (int shift = KeyBits<T>::value - 8; shift >= 0; shift -= 8) {
+    for (;;) {
+        uint32_t mx = 0u, mn = ~0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool in = ok[i] && (key[i] & pmask) == thr;
+            mx = in && key[i] > mx ? key[i] : mx;
+            mn = in && key[i] < mn ? key[i] : mn;
+        }
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) {
+            const uint32_t a = __shfl_xor(mx, off), b = __shfl_xor(mn, off);
+            mx = a > mx ? a : mx;
+            mn = b < mn ? b : mn;
+        }
+        const uint32_t diff = mx ^ mn;
+        if (diff == 0u) {  // every key in play is equal: it is T, ties decide
+            thr = mx;
+            sh = 0;
+            break;
+        }
+        const int hb = 31 - __builtin_clz(diff);  // highest bit where keys in play differ
+        const int shift = hb >= 7 ? hb - 7 : 0;   // digit = bits [shift, shift + 8)
         reinterpret_cast<uint4 *>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_fence();
 #pragma unroll
-        for (int i = 0; i < 4; ++i)  // branch-free: non-matching keys add 0
+        for (int i = 0; i < 4; ++i)  // branch-free: keys out of play add 0
             atomicAdd(&hist[(key[i] >> shift) & 255u], (ok[i] && (key[i] & pmask) == thr) ? 1u : 0u);
         wave_lds_fence();
         const uint4 h = reinterpret_cast<const uint4 *>(hist)[lane];  // bins 4*lane .. 4*lane+3
@@ -123,10 +142,12 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
         const uint32_t gt = __shfl(gt_l, src);
         const uint32_t in_bin = __shfl(ge_l, src) - gt;
         need -= (int)gt;
-        thr |= (uint32_t)(4 * src + dm) << shift;
-        pmask |= 255u << shift;
+        // keys in play share every bit above shift + 8 (they differ first at bit hb)
+        const uint32_t high = shift + 8 >= 32 ? 0u : (mx & (~0u << (shift + 8)));
+        thr = high | ((uint32_t)(4 * src + dm) << shift);
+        pmask = ~0u << shift;
         sh = shift;
-        if (in_bin == (uint32_t)need) break;  // the whole bin is taken: no lower digit matters
+        if (in_bin == (uint32_t)need || shift == 0) break;  // bin fully taken, or T exact
     }
     const int need_eq = need;
     thr >>= sh;
