@@ -20,11 +20,11 @@ forward and a reduce-scatter of the CBSR-gradient partials after the backward
 from __future__ import annotations
 
 import argparse
-import warnings
 import json
 import os
 import sys
 import time
+import warnings
 
 import numpy as np
 import torch
@@ -36,9 +36,6 @@ import maxk_graph  # noqa: E402
 warnings.filterwarnings("ignore", message="Sparse CSR tensor support")
 METRIC = "SpGEMM+SSpMM GTEPS (edges/s) & HBM-BW% on Reddit h=256 k=16; vs CPU SpMM"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-
-
-
 
 # kernels making up each op of one step (rocprofv3 names, maxk:: namespace)
 OP_KERNELS = {

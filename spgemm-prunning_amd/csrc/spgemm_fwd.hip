@@ -35,13 +35,19 @@ namespace {
 
 // Record stride: one power-of-two slot per vertex while the record
 // [k f32 | k u16 selectors] fits a 128-B line, else whole lines.
-inline int record_stride(int k) {
+// Past one line: whole 64-B sectors while the table stays well inside the 256 MiB
+// Infinity Cache (a smaller cache-resident table: Reddit k=32 3.60 -> 3.49 ms), whole
+// 128-B lines once it does not (every gather is then a random HBM request per line and
+// line-aligned records measured better: products k=32 6.53 -> 6.40 ms).
+inline int record_stride(int k, int64_t num_cols) {
     const int b = 6 * k;
     if (b <= 128) {
         int s = 16;
         while (s < b) s <<= 1;
         return s;
     }
+    const int s64 = (b + 63) / 64 * 64;
+    if ((int64_t)s64 * num_cols <= (128LL << 20)) return s64;
     return (b + 127) / 128 * 128;
 }
 
@@ -268,7 +274,7 @@ FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, i
     L.chunk = fwd_chunk(num_rows, num_e, chunk);
     const int64_t n = ceil_div(num_rows + num_e, L.chunk);
     L.n_items = (int)(n > 0 ? n : 1);
-    L.RS = record_stride(k);
+    L.RS = record_stride(k, num_cols);
     L.DS = copy_stride(D);
     L.kg = fwd_lanes_per_edge(k);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
