@@ -163,6 +163,9 @@ int maxk_dense_spmm_plan_create(maxk_dense_spmm_plan **plan, const int32_t *row_
                                 float *y, int64_t num_rows, int64_t num_cols, int64_t num_e,
                                 int32_t dim, int32_t alg, void *stream);
 int maxk_dense_spmm_run(maxk_dense_spmm_plan *plan, void *stream);
+/* Point the plan at new X / Y buffers of the same shape (one plan per graph serves every
+ * call, as cusparseSpMM's descriptors do in the reference's callers). */
+int maxk_dense_spmm_bind(maxk_dense_spmm_plan *plan, const float *x, float *y);
 int maxk_dense_spmm_plan_destroy(maxk_dense_spmm_plan *plan);
 
 #ifdef __cplusplus

@@ -109,6 +109,17 @@ extern "C" int maxk_dense_spmm_run(maxk_dense_spmm_plan *plan, void *stream) {
     return spmm_stage(plan, rocsparse_spmm_stage_compute, &plan->buffer_size, plan->buffer);
 }
 
+extern "C" int maxk_dense_spmm_bind(maxk_dense_spmm_plan *plan, const float *x, float *y) {
+    maxk::clear_error();
+    MAXK_REQUIRE(plan != nullptr && x != nullptr && y != nullptr, "NULL plan / x / y");
+    if (rocsparse_dnmat_set_values(plan->X, const_cast<float *>(x)) != rocsparse_status_success ||
+        rocsparse_dnmat_set_values(plan->Y, y) != rocsparse_status_success) {
+        maxk::set_error("rocsparse_dnmat_set_values failed");
+        return MAXK_ERR_LIBRARY;
+    }
+    return MAXK_OK;
+}
+
 extern "C" int maxk_dense_spmm_plan_destroy(maxk_dense_spmm_plan *plan) {
     destroy(plan);
     return MAXK_OK;

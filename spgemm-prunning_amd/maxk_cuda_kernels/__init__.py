@@ -446,7 +446,19 @@ class DenseSpMMPlan:
                 _stream(self.device)), "maxk_dense_spmm_plan_create")
         self._h = h
 
-    def run(self) -> torch.Tensor:
+    def run(self, x: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None
+            ) -> torch.Tensor:
+        """Y = A . X on the current stream; `x` / `y` rebind the dense operands (same shapes)."""
+        if x is not None or y is not None:
+            x = self.x if x is None else x
+            y = self.y if y is None else y
+            _need(x, "x", torch.float32)
+            _need(y, "y", torch.float32)
+            if tuple(x.shape) != tuple(self.x.shape) or tuple(y.shape) != tuple(self.y.shape):
+                raise RuntimeError("rebound x / y must keep the plan's shapes")
+            _capi.check(_lib().maxk_dense_spmm_bind(self._h, _ptr(x), _ptr(y)),
+                        "maxk_dense_spmm_bind")
+            self.x, self.y = x, y
         with torch.cuda.device(self.device):
             _capi.check(_lib().maxk_dense_spmm_run(self._h, _stream(self.device)),
                         "maxk_dense_spmm_run")

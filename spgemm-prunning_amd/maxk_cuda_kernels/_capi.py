@@ -49,6 +49,7 @@ SIGNATURES = {
     "maxk_dense_spmm_plan_create": (ctypes.c_int, [ctypes.POINTER(_p), _p, _p, _p, _p, _p,
                                                    _i64, _i64, _i64, _i32, _i32, _p]),
     "maxk_dense_spmm_run": (ctypes.c_int, [_p, _p]),
+    "maxk_dense_spmm_bind": (ctypes.c_int, [_p, _p, _p]),
     "maxk_dense_spmm_plan_destroy": (ctypes.c_int, [_p]),
 }
 

@@ -136,3 +136,14 @@ def test_sage_model_training_step(cuda):
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < 0.8 * losses[0], losses
+
+
+@pytest.mark.gpu
+def test_train_bench_matches_library(cuda):
+    """One epoch of the 3-layer MaxK-SAGE on the HIP aggregation and on rocSPARSE
+    (torch.sparse CSR): same first loss (BASELINE configs[2] driver, small graph)."""
+    import maxk_train_bench
+    out = maxk_train_bench.main(["flickr", "--hidden", "64", "--k", "16", "--epochs", "1",
+                                 "--warmup", "1"])
+    assert out["loss_match"], out
+    assert out["maxk_epoch_ms"] > 0 and out["library_epoch_ms"] > 0
