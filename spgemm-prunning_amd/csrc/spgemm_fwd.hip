@@ -58,36 +58,58 @@ inline int fwd_lanes_per_edge(int k) {
     return g < 8 ? 8 : g;
 }
 
-// One thread per (vertex, l).  Duplicate selectors of a vertex: the first
-// occurrence (lowest l) carries the sum of their values, the others point at
-// the trash column `trash` with value 0.  Selectors >= D also go to trash.
+// Packs the records of groups of whole vertices (vpw = min(32, 256 / k) per
+// workgroup, one thread per (vertex, l)), grid-stride: a launch of one small
+// workgroup per 256 (vertex, l) pairs is bound by workgroup dispatch (products
+// k=32: 306k workgroups, 1.65 ms).  Duplicate selectors of a vertex: the first
+// occurrence (lowest l, found with an LDS atomicMin per (vertex, selector))
+// carries the sum of their values in l order, the others point at the trash
+// column `trash` with value 0.  Selectors >= D also go to trash.
+constexpr int kPackMaxV = 32;  // vertices per group (LDS: 32 x 256 first-occurrence slots)
+
 __global__ __launch_bounds__(kBlock) void cbsr_pack_kernel(const float *__restrict__ cbsr_val,
                                                            const uint8_t *__restrict__ cbsr_idx,
                                                            uint8_t *__restrict__ rec, int num_cols,
                                                            int k, int RS, int D, int trash) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)num_cols * k) return;
-    const int64_t v = i / k;
-    const int l = (int)(i - v * k);
-    const uint8_t *sv = cbsr_idx + v * k;
-    const float *dv = cbsr_val + v * k;
-    const int s = sv[l];
-    float val = dv[l];
-    int out_s = s < D ? s : trash;
-    if (out_s != trash) {
-        for (int j = 0; j < l; ++j)
-            if (sv[j] == s) {
-                out_s = trash;
-                break;
-            }
-        if (out_s != trash) {
-            for (int j = l + 1; j < k; ++j)
-                if (sv[j] == s) val += dv[j];
+    __shared__ uint32_t s_first[kPackMaxV][256];
+    __shared__ uint8_t s_sel[kBlock];
+    __shared__ float s_val[kBlock];
+    __shared__ int s_dup[kPackMaxV];
+    const int vpw = k >= kBlock / kPackMaxV ? kBlock / k : kPackMaxV;
+    const int t = threadIdx.x;
+    const int vl = t / k, l = t - vl * k;
+    for (int64_t g0 = (int64_t)blockIdx.x * vpw; g0 < num_cols; g0 += (int64_t)gridDim.x * vpw) {
+        const int64_t v = g0 + vl;
+        const bool act = vl < vpw && v < num_cols;
+        int s = 0;
+        float val = 0.f;
+        if (act) {
+            s = cbsr_idx[v * k + l];
+            val = cbsr_val[v * k + l];
+            s_sel[t] = (uint8_t)s;
+            s_val[t] = val;
+            s_first[vl][s] = 0xffffffffu;
         }
+        if (t < vpw) s_dup[t] = 0;
+        __syncthreads();
+        if (act) atomicMin(&s_first[vl][s], (uint32_t)l);
+        __syncthreads();
+        const bool first = act && s_first[vl][s] == (uint32_t)l;
+        if (act && !first) s_dup[vl] = 1;
+        __syncthreads();
+        if (act) {
+            float outv = val;
+            if (first && s_dup[vl]) {  // rare: fold the later duplicates, in l order
+                for (int j = l + 1; j < k; ++j)
+                    if (s_sel[vl * k + j] == s) outv += s_val[vl * k + j];
+            }
+            const bool keep = first && s < D;
+            uint8_t *p = rec + v * RS;
+            reinterpret_cast<float *>(p)[l] = keep ? outv : 0.f;
+            reinterpret_cast<uint16_t *>(p + 4 * k)[l] = (uint16_t)(keep ? s : trash);
+        }
+        __syncthreads();  // LDS is reused by the next group
     }
-    uint8_t *p = rec + v * RS;
-    reinterpret_cast<float *>(p)[l] = out_s == trash ? 0.f : val;
-    reinterpret_cast<uint16_t *>(p + 4 * k)[l] = (uint16_t)out_s;
 }
 
 template <int KG, int U>
@@ -346,8 +368,10 @@ extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_id
     hipStream_t s = as_stream(stream);
     const int D = dim_origin, k = dim_k;
     if (num_cols > 0) {
-        const int64_t n = num_cols * k;
-        hipLaunchKernelGGL(cbsr_pack_kernel, dim3((unsigned)ceil_div(n, kBlock)), dim3(kBlock), 0,
+        const int vpw = k >= kBlock / kPackMaxV ? kBlock / k : kPackMaxV;
+        const int64_t groups = ceil_div(num_cols, (int64_t)vpw);
+        hipLaunchKernelGGL(cbsr_pack_kernel, dim3((unsigned)(groups < 4096 ? groups : 4096)),
+                           dim3(kBlock), 0,
                            s, cbsr_val, cbsr_idx, rec, (int)num_cols, k, L.RS, D, L.DS - 1);
         MAXK_LAUNCHED("cbsr_pack_kernel");
     }

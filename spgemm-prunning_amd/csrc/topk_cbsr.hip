@@ -196,26 +196,29 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
     }
 }
 
-// dense[r, :] = 0; dense[r, idx[r, l]] = val[r, l]   (one wave per row)
+// dense[r, :] = 0; dense[r, idx[r, l]] = val[r, l]   (one wave per row, grid-stride: one
+// workgroup per 4 rows would be bound by workgroup dispatch on large graphs)
 __global__ __launch_bounds__(kBlock) void cbsr_scatter_dense_kernel(
     const float *__restrict__ val, const uint8_t *__restrict__ idx, float *__restrict__ dense,
     int num_rows, int D, int k) {
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kMaxDim];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int row = blockIdx.x * kWavesPerBlock + wid;
-    if (row >= num_rows) return;
     float *buf = lds[wid];
-    *reinterpret_cast<float4 *>(&buf[lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
-    wave_lds_fence();
-    for (int l = lane; l < k; l += kWave) buf[idx[(int64_t)row * k + l]] = val[(int64_t)row * k + l];
-    wave_lds_fence();
-    float *dst = dense + (int64_t)row * D;
-    if ((D & 3) == 0) {
-        for (int j = lane * 4; j < D; j += kWave * 4)
-            *reinterpret_cast<float4 *>(&dst[j]) = *reinterpret_cast<const float4 *>(&buf[j]);
-    } else {
-        for (int j = lane; j < D; j += kWave) dst[j] = buf[j];
+    for (int row = blockIdx.x * kWavesPerBlock + wid; row < num_rows;
+         row += gridDim.x * kWavesPerBlock) {
+        *reinterpret_cast<float4 *>(&buf[lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+        wave_lds_fence();
+        for (int l = lane; l < k; l += kWave) buf[idx[(int64_t)row * k + l]] = val[(int64_t)row * k + l];
+        wave_lds_fence();
+        float *dst = dense + (int64_t)row * D;
+        if ((D & 3) == 0) {
+            for (int j = lane * 4; j < D; j += kWave * 4)
+                *reinterpret_cast<float4 *>(&dst[j]) = *reinterpret_cast<const float4 *>(&buf[j]);
+        } else {
+            for (int j = lane; j < D; j += kWave) dst[j] = buf[j];
+        }
+        wave_lds_fence();
     }
 }
 
@@ -265,7 +268,8 @@ extern "C" int maxk_cbsr_scatter_dense(const float *cbsr_val, const uint8_t *cbs
     MAXK_REQUIRE(dim_k >= 1 && dim_k <= dim_origin, "dim_k must be in [1,dim_origin]");
     if (num_rows == 0) return MAXK_OK;
     MAXK_REQUIRE(cbsr_val && cbsr_idx && dense, "pointers must not be NULL");
-    const dim3 grid((unsigned)ceil_div(num_rows, kWavesPerBlock));
+    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
+    const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
     hipLaunchKernelGGL(cbsr_scatter_dense_kernel, grid, dim3(kBlock), 0, as_stream(stream),
                        cbsr_val, cbsr_idx, dense, (int)num_rows, dim_origin, dim_k);
     MAXK_LAUNCHED("cbsr_scatter_dense_kernel");
