@@ -150,4 +150,56 @@ __device__ __forceinline__ int wave_first_row_token(const int32_t *__restrict__ 
     return r > hi ? hi : r;
 }
 
+
+// ---- split-row fixup shared by the forward (TAG 0) and the backward's phase 2 (TAG 1) ----
+// out[row, 0:width] += slab[i, 0:width] for every run of consecutive items i whose
+// slab_row[i] == row (a row split over items), added in item order: deterministic.  16
+// lanes per item (4 items per wave): one wave per item made the launch bound by workgroup
+// dispatch (65k items -> 16k workgroups), while most items do carry a slab, so every head
+// must still run in parallel.  TAG only separates the two ops in profiles.
+namespace {
+template <int TAG>
+__global__ __launch_bounds__(kBlock) void slab_fixup_kernel(const float *__restrict__ slab,
+                                                            const int32_t *__restrict__ slab_row,
+                                                            float *__restrict__ out, int width,
+                                                            int n_items) {
+    const int item = (int)((blockIdx.x * (int64_t)kBlock + threadIdx.x) / 16);
+    const int g = threadIdx.x % 16;
+    if (item >= n_items) return;
+    const int row = slab_row[item];
+    if (row < 0 || (item > 0 && slab_row[item - 1] == row)) return;
+    float *o = out + (int64_t)row * width;
+    if ((width & 3) == 0) {
+        for (int j = g * 4; j < width; j += 64) {
+            float4 a = *reinterpret_cast<const float4 *>(o + j);
+            for (int i = item; i < n_items && slab_row[i] == row; ++i) {
+                const float4 b = *reinterpret_cast<const float4 *>(slab + (int64_t)i * width + j);
+                a.x += b.x;
+                a.y += b.y;
+                a.z += b.z;
+                a.w += b.w;
+            }
+            *reinterpret_cast<float4 *>(o + j) = a;
+        }
+    } else {
+        for (int j = g; j < width; j += 16) {
+            float a = o[j];
+            for (int i = item; i < n_items && slab_row[i] == row; ++i)
+                a += slab[(int64_t)i * width + j];
+            o[j] = a;
+        }
+    }
+}
+}  // namespace
+
+template <int TAG>
+inline int launch_slab_fixup(const float *slab, const int32_t *slab_row, float *out, int width,
+                             int n_items, hipStream_t s) {
+    if (n_items <= 0) return MAXK_OK;
+    hipLaunchKernelGGL(slab_fixup_kernel<TAG>, dim3((unsigned)ceil_div(n_items, kBlock / 16)),
+                       dim3(kBlock), 0, s, slab, slab_row, out, width, n_items);
+    MAXK_LAUNCHED("slab_fixup_kernel");
+    return MAXK_OK;
+}
+
 }  // namespace maxk

@@ -26,7 +26,7 @@
 //       (copies summed in fixed order, divided by row_div, 16-B stores): no
 //       zero-init of `out`, no global atomics.  A hub row continued from the
 //       previous item goes to a per-item slab.
-//  3. spgemm_fwd_fixup_kernel adds the slabs of each split row in item order
+//  3. slab_fixup_kernel<0> (common.h) adds the slabs of each split row in item order
 //     (deterministic) onto the owner's partial.
 #include "common.h"
 
@@ -254,25 +254,6 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     }
 }
 
-// out[row] += sum of the slabs of split rows, in item order.  One wave per item;
-// only the first item of each run of equal slab_row does the work.
-__global__ __launch_bounds__(kBlock) void spgemm_fwd_fixup_kernel(
-    const float *__restrict__ slab, const int32_t *__restrict__ slab_row, float *__restrict__ out,
-    int D, int n_items) {
-    const int wid = threadIdx.x / kWave;
-    const int lane = lane_id();
-    const int item = blockIdx.x * kWavesPerBlock + wid;
-    if (item >= n_items) return;
-    const int row = slab_row[item];
-    if (row < 0) return;
-    if (item > 0 && slab_row[item - 1] == row) return;
-    for (int j = lane; j < D; j += kWave) {
-        float a = out[(int64_t)row * D + j];
-        for (int i = item; i < n_items && slab_row[i] == row; ++i) a += slab[(int64_t)i * D + j];
-        out[(int64_t)row * D + j] = a;
-    }
-}
-
 int fwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk) {
     if (chunk > 0) return chunk;
     // ~8 waves of work per resident wave slot on 256 CUs, within [256, 2048] tokens
@@ -392,8 +373,5 @@ extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_id
             return MAXK_ERR_INVALID;
     }
     MAXK_LAUNCHED("spgemm_fwd_kernel");
-    hipLaunchKernelGGL(spgemm_fwd_fixup_kernel, dim3((unsigned)ceil_div(L.n_items, kWavesPerBlock)),
-                       dim3(kBlock), 0, s, slab, slab_row, out, D, L.n_items);
-    MAXK_LAUNCHED("spgemm_fwd_fixup_kernel");
-    return MAXK_OK;
+    return launch_slab_fixup<0>(slab, slab_row, out, D, L.n_items, s);
 }

@@ -395,25 +395,6 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
     }
 }
 
-// grad_cbsr[row] += slabs of the split destination rows, in item order.
-__global__ __launch_bounds__(kBlock) void csc_sum_fixup_kernel(const float *__restrict__ slab,
-                                                               const int32_t *__restrict__ slab_row,
-                                                               float *__restrict__ out, int k,
-                                                               int n_items) {
-    const int wid = threadIdx.x / kWave;
-    const int lane = lane_id();
-    const int item = blockIdx.x * kWavesPerBlock + wid;
-    if (item >= n_items) return;
-    const int row = slab_row[item];
-    if (row < 0) return;
-    if (item > 0 && slab_row[item - 1] == row) return;
-    for (int j = lane; j < k; j += kWave) {
-        float a = out[(int64_t)row * k + j];
-        for (int i = item; i < n_items && slab_row[i] == row; ++i) a += slab[(int64_t)i * k + j];
-        out[(int64_t)row * k + j] = a;
-    }
-}
-
 // Auto item size: ~`per_slot` items per resident wave slot on 256 CUs, in [256, 2048].
 int bwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int per_slot) {
     if (chunk > 0) return chunk;
@@ -649,8 +630,5 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
         }
     }
     MAXK_LAUNCHED("csc_sum_kernel");
-    hipLaunchKernelGGL(csc_sum_fixup_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, slab,
-                       slab_row, grad_cbsr, k, L.n_items);
-    MAXK_LAUNCHED("csc_sum_fixup_kernel");
-    return MAXK_OK;
+    return launch_slab_fixup<1>(slab, slab_row, grad_cbsr, k, L.n_items, s);
 }

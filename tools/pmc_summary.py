@@ -26,7 +26,10 @@ def short(n):
 
 
 def base(n):
-    return short(n).replace("maxk::", "").split("<")[0]
+    """Kernel name without namespace; template arguments dropped except where they tell
+    two ops apart (slab_fixup_kernel<0> forward, <1> backward)."""
+    n = short(n).replace("maxk::", "")
+    return n if n.startswith("slab_fixup_kernel<") else n.split("<")[0]
 
 
 def main():

@@ -15,8 +15,11 @@ from bench import OP_KERNELS  # noqa: E402
 
 
 def base(n):
+    """Kernel name without namespace; template arguments dropped except where they tell
+    two ops apart (slab_fixup_kernel<0> forward, <1> backward)."""
     n = n.replace("void ", "").replace("(anonymous namespace)::", "")
-    return n.split("(")[0].replace("maxk::", "").split("<")[0]
+    n = n.split("(")[0].replace("maxk::", "")
+    return n if n.startswith("slab_fixup_kernel<") else n.split("<")[0]
 
 
 def main(stats, bench=None):
