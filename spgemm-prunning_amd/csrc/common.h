@@ -12,7 +12,7 @@
 namespace maxk {
 
 constexpr int kWave = 64;          // CDNA wavefront
-constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr int kBlock = 256;        // threads per workgroup (4 waves; 512 / 1024 measured slower)
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows are 256 floats
 
@@ -50,6 +50,9 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #endif
 #ifndef MAXK_P2_ITEMS
 #define MAXK_P2_ITEMS 16
+#endif
+#ifndef MAXK_PACK_GRID  // grid cap of the grid-stride record pack
+#define MAXK_PACK_GRID 4096
 #endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
