@@ -1,0 +1,13 @@
+#!/bin/bash
+# Every committed measurement of a round: gpu_round (tests, smoke, bench, stats, PMC), the
+# presets (+ training epochs, products k sweep) and the reference-style kernel test.
+set -e
+R=${1:-r01}
+bash tools/gpu_round.sh $R
+bash tools/run_presets.sh > gpurun_out/presets_stdout.txt 2>&1
+mkdir -p gpurun_out/kt
+for g in reddit products proteins; do
+  timeout -k 10 300 python spgemm-prunning_amd/maxk_kernel_test.py $g --k 8 16 32 64 --json > gpurun_out/kt/$g.txt 2> gpurun_out/kt/$g.err
+done
+timeout -k 10 300 python spgemm-prunning_amd/maxk_kernel_test.py flickr --dim 64 --k 8 16 32 64 --json > gpurun_out/kt/flickr.txt 2> gpurun_out/kt/flickr.err
+echo refresh done
