@@ -340,6 +340,8 @@ def main():
 
     extra = {
         "fwd_ms": round(fwd_avg, 4), "bwd_ms": round(bwd_avg, 4),
+        "fwd_ms_median": round(float(np.median(fwd_ms)), 4),
+        "bwd_ms_median": round(float(np.median(bwd_ms)), 4),
         "fwd_gteps": round(El / fwd_avg / 1e6, 3), "bwd_gteps": round(El / bwd_avg / 1e6, 3),
         "fwd_alg_GBs": round(B_f / fwd_avg / 1e6, 1), "bwd_alg_GBs": round(B_b / bwd_avg / 1e6, 1),
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
