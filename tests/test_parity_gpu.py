@@ -355,6 +355,32 @@ def test_hipgraph_capture(mk, cuda):
     close(out, z["y_ref"])
 
 
+def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch):
+    """Default (validate-once) mode: the first call may be inside a capture; forward and the
+    deterministic backward (with its plan built beforehand) both replay correctly."""
+    monkeypatch.setenv("MAXK_VALIDATE", "")
+    z = load_golden(CASES[2])
+    rp, ci, va, cv, cs = [T(z[n], cuda).clone() for n in ("row_ptr", "col_idx", "val", "topk_val",
+                                                         "topk_idx")]
+    deg, g_in = T(z["deg"], cuda), T(z["g"], cuda)
+    D = int(z["D"])
+    V = rp.numel() - 1
+    out = torch.empty(V, D, device=cuda)
+    gs = torch.empty(cs.shape, device=cuda)
+    plan = mk.transpose_plan(ci, cs.shape[0])
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        mk.spgemm_forward(rp, ci, va, cv, cs, D, row_div=deg, out=out)
+        mk.sspmm_backward(rp, ci, va, g_in, cs, row_div=deg, out=gs, plan=plan, mode="csc")
+    out.fill_(float("nan"))
+    gs.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    close(out, z["y_ref"])
+    close(gs, z["grad_cbsr_ref"])
+
+
 # --------------------------------------------------------------------------- size-independent
 def test_adjoint_identity_large(mk, cuda):
     """<fwd(v), G> == <v, bwd(G)> on a 2M-edge power-law graph (no oracle needed)."""
