@@ -131,6 +131,25 @@ int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_val, uint8_t
 int maxk_cbsr_scatter_dense(const float *cbsr_val, const uint8_t *cbsr_idx, float *dense,
                             int64_t num_rows, int32_t dim_origin, int32_t dim_k, void *stream);
 
+/* Fused MaxK activation, forward: maxk_topk_cbsr plus the masked dense output
+ * dense[r, j] = x[r, j] if j is among row r's k winners, else 0 (row stride dim_origin),
+ * written by the same kernel from the row it already holds.
+ * Replaces: MaxK.forward, topk + zeros_like + scatter_ (model_integrated_v3.py:28-38),
+ *           i.e. the top-k pass plus two dense V x D passes. */
+int maxk_topk_cbsr_dense(const float *x, int64_t ld_x, float *cbsr_val, uint8_t *cbsr_idx,
+                         float *dense, int64_t num_rows, int32_t dim_origin, int32_t dim_k,
+                         void *stream);
+
+/* Fused MaxK activation, backward, in one pass over the rows:
+ *   grad_x[r, :] = 0;  grad_x[r, j] = grad_val[r, l] + grad_dense[r, j]  for j = cbsr_idx[r, l].
+ * grad_val [V,k] and grad_dense [V,D] are each optional (NULL = zero); grad_x may alias
+ * grad_dense.  Selectors of a row are distinct (top-k output); with duplicates one of them wins.
+ * Replaces: OPTMaxK.backward's mask multiply (model_integrated_v3.py:39-43) together with
+ *           zeros(V,D).scatter_(1, sel, grad_sparse) (maxk_spgemm_function.py:152,175). */
+int maxk_topk_backward(const float *grad_val, const float *grad_dense, const uint8_t *cbsr_idx,
+                       float *grad_x, int64_t num_rows, int32_t dim_origin, int32_t dim_k,
+                       void *stream);
+
 /* ---------------------------------------------------------------------------
  * warp4 schedule (drop-in for kernels/generate_meta.py:30-48 / generate_meta_csc.py:14-93
  * and the .warp4 files read by load_warp4_metadata, cuda_kernel_bindings.cpp:287-317).

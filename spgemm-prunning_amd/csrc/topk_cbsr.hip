@@ -35,6 +35,7 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
                                                            T *__restrict__ out_val,
                                                            uint8_t *__restrict__ out_idx,
                                                            int32_t *__restrict__ out_idx32,
+                                                           T *__restrict__ out_dense,
                                                            int num_rows, int D, int k) {
     // winner slots [0, k), padding slots [k, k4) (key 0, column 255: never ranked above a
     // winner), and per-lane scratch slots [kMaxDim, kMaxDim + 64) for lanes not taking
@@ -166,6 +167,8 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
         const int eq_rank = eq_base + __popcll(me & lt_mask);
         eq_base += __popcll(me);
         const bool take = (ok[i] && (key[i] >> sh) > thr) || (eq && eq_rank < need_eq);
+        if (out_dense && ok[i])  // fused masked dense output (wave-uniform pointer test)
+            out_dense[(int64_t)row * D + lane + kWave * i] = take ? v[i] : T(0);
         const uint64_t mt = __ballot(take);
         const int slot = take ? slot_base + __popcll(mt & lt_mask) : kMaxDim + lane;
         s_key[wid][slot] = key[i];
@@ -196,11 +199,13 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
     }
 }
 
-// dense[r, :] = 0; dense[r, idx[r, l]] = val[r, l]   (one wave per row, grid-stride: one
-// workgroup per 4 rows would be bound by workgroup dispatch on large graphs)
+// dense[r, :] = 0; dense[r, idx[r, l]] = val[r, l] + add[r, idx[r, l]]   (val and add
+// optional).  One wave per row, grid-stride: one workgroup per 4 rows would be bound by
+// workgroup dispatch on large graphs.  A row's reads all land in LDS before its stores, so
+// dense may alias add (in-place MaxK gradient).
 __global__ __launch_bounds__(kBlock) void cbsr_scatter_dense_kernel(
-    const float *__restrict__ val, const uint8_t *__restrict__ idx, float *__restrict__ dense,
-    int num_rows, int D, int k) {
+    const float *__restrict__ val, const uint8_t *__restrict__ idx, const float *add,
+    float *dense, int num_rows, int D, int k) {
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kMaxDim];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
@@ -209,7 +214,12 @@ __global__ __launch_bounds__(kBlock) void cbsr_scatter_dense_kernel(
          row += gridDim.x * kWavesPerBlock) {
         *reinterpret_cast<float4 *>(&buf[lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
         wave_lds_fence();
-        for (int l = lane; l < k; l += kWave) buf[idx[(int64_t)row * k + l]] = val[(int64_t)row * k + l];
+        for (int l = lane; l < k; l += kWave) {
+            const int j = idx[(int64_t)row * k + l];
+            float x = val ? val[(int64_t)row * k + l] : 0.f;
+            if (add) x += add[(int64_t)row * D + j];
+            buf[j] = x;
+        }
         wave_lds_fence();
         float *dst = dense + (int64_t)row * D;
         if ((D & 3) == 0) {
@@ -223,8 +233,8 @@ __global__ __launch_bounds__(kBlock) void cbsr_scatter_dense_kernel(
 }
 
 template <typename T>
-int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, int64_t num_rows,
-                int32_t D, int32_t k, void *stream) {
+int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, T *dense,
+                int64_t num_rows, int32_t D, int32_t k, void *stream) {
     clear_error();
     MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
     MAXK_REQUIRE(D >= 1 && D <= kMaxDim, "dim_origin must be in [1,256], got %d", D);
@@ -235,7 +245,7 @@ int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, 
     const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
     const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
     hipLaunchKernelGGL(topk_cbsr_kernel<T>, grid, dim3(kBlock), 0, as_stream(stream), x, ld_x, val,
-                       idx, idx32, (int)num_rows, D, k);
+                       idx, idx32, dense, (int)num_rows, D, k);
     MAXK_LAUNCHED("topk_cbsr_kernel");
     return MAXK_OK;
 }
@@ -248,30 +258,59 @@ using namespace maxk;
 extern "C" int maxk_topk_cbsr(const float *x, int64_t ld_x, float *cbsr_val, uint8_t *cbsr_idx,
                               int32_t *idx32, int64_t num_rows, int32_t dim_origin, int32_t dim_k,
                               void *stream) {
-    return topk_launch<float>(x, ld_x, cbsr_val, cbsr_idx, idx32, num_rows, dim_origin, dim_k,
-                              stream);
+    return topk_launch<float>(x, ld_x, cbsr_val, cbsr_idx, idx32, nullptr, num_rows, dim_origin,
+                              dim_k, stream);
+}
+
+extern "C" int maxk_topk_cbsr_dense(const float *x, int64_t ld_x, float *cbsr_val,
+                                    uint8_t *cbsr_idx, float *dense, int64_t num_rows,
+                                    int32_t dim_origin, int32_t dim_k, void *stream) {
+    if (num_rows > 0 && !dense) {
+        clear_error();
+        MAXK_REQUIRE(dense, "dense must not be NULL");
+    }
+    return topk_launch<float>(x, ld_x, cbsr_val, cbsr_idx, nullptr, dense, num_rows, dim_origin,
+                              dim_k, stream);
 }
 
 extern "C" int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_val,
                                  uint8_t *cbsr_idx, int32_t *idx32, int64_t num_rows,
                                  int32_t dim_origin, int32_t dim_k, void *stream) {
-    return topk_launch<uint8_t>(x, ld_x, cbsr_val, cbsr_idx, idx32, num_rows, dim_origin, dim_k,
-                                stream);
+    return topk_launch<uint8_t>(x, ld_x, cbsr_val, cbsr_idx, idx32, nullptr, num_rows, dim_origin,
+                                dim_k, stream);
+}
+
+namespace maxk {
+namespace {
+int scatter_launch(const float *val, const uint8_t *idx, const float *add, float *dense,
+                   int64_t num_rows, int32_t dim_origin, int32_t dim_k, void *stream) {
+    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
+    MAXK_REQUIRE(dim_origin >= 1 && dim_origin <= kMaxDim, "dim_origin must be in [1,256]");
+    MAXK_REQUIRE(dim_k >= 1 && dim_k <= dim_origin, "dim_k must be in [1,dim_origin]");
+    if (num_rows == 0) return MAXK_OK;
+    MAXK_REQUIRE(idx && dense, "pointers must not be NULL");
+    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
+    const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
+    hipLaunchKernelGGL(cbsr_scatter_dense_kernel, grid, dim3(kBlock), 0, as_stream(stream), val,
+                       idx, add, dense, (int)num_rows, dim_origin, dim_k);
+    MAXK_LAUNCHED("cbsr_scatter_dense_kernel");
+    return MAXK_OK;
+}
+}  // namespace
+}  // namespace maxk
+
+extern "C" int maxk_topk_backward(const float *grad_val, const float *grad_dense,
+                                  const uint8_t *cbsr_idx, float *grad_x, int64_t num_rows,
+                                  int32_t dim_origin, int32_t dim_k, void *stream) {
+    clear_error();
+    return scatter_launch(grad_val, cbsr_idx, grad_dense, grad_x, num_rows, dim_origin, dim_k,
+                          stream);
 }
 
 extern "C" int maxk_cbsr_scatter_dense(const float *cbsr_val, const uint8_t *cbsr_idx,
                                        float *dense, int64_t num_rows, int32_t dim_origin,
                                        int32_t dim_k, void *stream) {
     clear_error();
-    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
-    MAXK_REQUIRE(dim_origin >= 1 && dim_origin <= kMaxDim, "dim_origin must be in [1,256]");
-    MAXK_REQUIRE(dim_k >= 1 && dim_k <= dim_origin, "dim_k must be in [1,dim_origin]");
-    if (num_rows == 0) return MAXK_OK;
-    MAXK_REQUIRE(cbsr_val && cbsr_idx && dense, "pointers must not be NULL");
-    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
-    const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
-    hipLaunchKernelGGL(cbsr_scatter_dense_kernel, grid, dim3(kBlock), 0, as_stream(stream),
-                       cbsr_val, cbsr_idx, dense, (int)num_rows, dim_origin, dim_k);
-    MAXK_LAUNCHED("cbsr_scatter_dense_kernel");
-    return MAXK_OK;
+    MAXK_REQUIRE(num_rows == 0 || cbsr_val, "cbsr_val must not be NULL");
+    return scatter_launch(cbsr_val, cbsr_idx, nullptr, dense, num_rows, dim_origin, dim_k, stream);
 }

@@ -37,7 +37,8 @@ __all__ = [
     "load_warp4_metadata_csc", "generate_sparse_selector", "benchmark_spmm_maxk",
     "validate_spmm_maxk", "validate_spmm_maxk_backward", "CudaTimer",
     # MI355X additions
-    "topk_cbsr", "cbsr_scatter_dense", "build_warp4_metadata", "warp4_to_indptr",
+    "topk_cbsr", "cbsr_scatter_dense", "topk_cbsr_dense", "topk_backward",
+    "build_warp4_metadata", "warp4_to_indptr",
     "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
     "transpose_plan",
 ]
@@ -414,6 +415,59 @@ def cbsr_scatter_dense(cbsr_val: torch.Tensor, cbsr_idx: torch.Tensor, dim_origi
         _capi.check(_lib().maxk_cbsr_scatter_dense(_ptr(cbsr_val), _ptr(cbsr_idx), _ptr(out), V,
                                                    dim_origin, k, _stream(dev)),
                     "maxk_cbsr_scatter_dense")
+    return out
+
+
+def topk_cbsr_dense(x: torch.Tensor, k: int):
+    """Fused MaxK forward: (dense masked x, values, uint8 indices) from one HIP kernel --
+    torch.topk + zeros_like + scatter_ of model_integrated_v3.py:28-38 in a single pass."""
+    if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32):
+        raise RuntimeError("x must be a float32 CUDA tensor")
+    if x.dim() != 2:
+        raise RuntimeError("Input must be 2D tensor")
+    if x.stride(1) != 1:
+        x = x.contiguous()
+    V, D = x.shape
+    if not (0 < k <= D):
+        raise RuntimeError("Invalid k value")
+    dev = x.device
+    val = torch.empty(V, k, dtype=torch.float32, device=dev)
+    idx = torch.empty(V, k, dtype=torch.uint8, device=dev)
+    dense = torch.empty(V, D, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(_lib().maxk_topk_cbsr_dense(_ptr(x), x.stride(0), _ptr(val), _ptr(idx),
+                                                _ptr(dense), V, D, k, _stream(dev)),
+                    "maxk_topk_cbsr_dense")
+    return dense, val, idx
+
+
+def topk_backward(grad_val: Optional[torch.Tensor], grad_dense: Optional[torch.Tensor],
+                  cbsr_idx: torch.Tensor, dim_origin: int,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused MaxK backward: grad_x = scatter(grad_val + grad_dense[sel]) over the selected
+    columns, zero elsewhere, in one HIP pass (OPTMaxK.backward, model_integrated_v3.py:39-43,
+    with the topk_values gradient it drops; maxk_spgemm_function.py:152,175)."""
+    _need(cbsr_idx, "cbsr_idx", torch.uint8)
+    V, k = cbsr_idx.shape
+    dev = cbsr_idx.device
+    if grad_val is not None:
+        _need(grad_val, "grad_val", torch.float32)
+        if tuple(grad_val.shape) != (V, k):
+            raise RuntimeError("grad_val must be [V, k]")
+    if grad_dense is not None:
+        _need(grad_dense, "grad_dense", torch.float32)
+        if tuple(grad_dense.shape) != (V, dim_origin):
+            raise RuntimeError("grad_dense must be [V, dim_origin]")
+    if out is None:
+        out = torch.empty(V, dim_origin, dtype=torch.float32, device=dev)
+    else:
+        _need(out, "out", torch.float32)
+        if tuple(out.shape) != (V, dim_origin):
+            raise RuntimeError("out must be [V, dim_origin]")
+    with torch.cuda.device(dev):
+        _capi.check(_lib().maxk_topk_backward(_ptr(grad_val), _ptr(grad_dense), _ptr(cbsr_idx),
+                                              _ptr(out), V, dim_origin, k, _stream(dev)),
+                    "maxk_topk_backward")
     return out
 
 

@@ -42,6 +42,8 @@ SIGNATURES = {
     "maxk_topk_cbsr": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_u8": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_cbsr_scatter_dense": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),
+    "maxk_topk_cbsr_dense": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
+    "maxk_topk_backward": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_warp4_count": (ctypes.c_int, [_p, _i64, _i32, ctypes.POINTER(_i64), _p]),
     "maxk_warp4_build_workspace_size": (_sz, [_i64]),
     "maxk_warp4_build": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _p, _sz, _p]),

@@ -113,18 +113,24 @@ class ShardedMaxK:
         self._plan = None
 
     # ---- helpers
-    def pad_rows(self, t: torch.Tensor) -> torch.Tensor:
-        out = torch.zeros((self.vmax,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        out[:t.shape[0]] = t
-        return out
-
     def gather_cbsr(self, val_local: torch.Tensor, idx_local: torch.Tensor):
-        """All-gather the CBSR rows of every shard into the padded [world*vmax, k] space."""
+        """All-gather the CBSR rows of every shard into the padded [world*vmax, k] space.
+
+        One collective: each rank sends one byte chunk [vmax*k values | vmax*k selectors]
+        (padding rows zero), so the values and selectors travel in a single all-gather
+        instead of two; the two halves are then split out of the gathered chunks."""
         k = val_local.shape[1]
-        val_all = torch.empty(self.n_cols, k, dtype=val_local.dtype, device=val_local.device)
-        idx_all = torch.empty(self.n_cols, k, dtype=idx_local.dtype, device=idx_local.device)
-        all_gather_rows(val_all, self.pad_rows(val_local).contiguous(), self.group)
-        all_gather_rows(idx_all, self.pad_rows(idx_local).contiguous(), self.group)
+        dev = val_local.device
+        nv = self.vmax * k
+        vb = nv * val_local.element_size()
+        chunk = vb + nv * idx_local.element_size()
+        send = torch.zeros(chunk, dtype=torch.uint8, device=dev)
+        send[:vb].view(val_local.dtype).view(self.vmax, k)[:self.n_local] = val_local
+        send[vb:].view(idx_local.dtype).view(self.vmax, k)[:self.n_local] = idx_local
+        recv = torch.empty(self.world, chunk, dtype=torch.uint8, device=dev)
+        all_gather_rows(recv.view(-1), send, self.group)
+        val_all = recv[:, :vb].contiguous().view(val_local.dtype).view(self.n_cols, k)
+        idx_all = recv[:, vb:].contiguous().view(idx_local.dtype).view(self.n_cols, k)
         return val_all, idx_all
 
     def plan(self):

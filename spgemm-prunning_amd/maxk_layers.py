@@ -65,13 +65,16 @@ class CSRGraph:
 class MaxK(Function):
     """MaxK nonlinearity (model_integrated_v3.py:28-60): keeps the k largest entries of each
     row.  Returns (dense masked output, topk_values, topk_indices u8); gradients from the
-    dense output and from topk_values both reach the input (the reference drops the latter)."""
+    dense output and from topk_values both reach the input (the reference drops the latter).
+
+    Both directions are single fused HIP passes: the forward writes the
+    CBSR and the masked dense row from one top-k kernel (maxk_topk_cbsr_dense); the backward
+    gathers the dense gradient at the selected columns, adds the topk_values gradient and
+    writes the whole dense row in one kernel (maxk_topk_backward)."""
 
     @staticmethod
     def forward(ctx, x: torch.Tensor, k: int):
-        x = x.float().contiguous()
-        vals, idx = mk.topk_cbsr(x, int(k))
-        dense = mk.cbsr_scatter_dense(vals, idx, x.shape[1])
+        dense, vals, idx = mk.topk_cbsr_dense(x.float(), int(k))
         ctx.save_for_backward(idx)
         ctx.D = x.shape[1]
         ctx.mark_non_differentiable(idx)
@@ -80,10 +83,9 @@ class MaxK(Function):
     @staticmethod
     def backward(ctx, g_dense, g_vals, g_idx):
         idx, = ctx.saved_tensors
-        g = torch.zeros(idx.shape, device=idx.device) if g_vals is None else g_vals.float()
-        if g_dense is not None:
-            g = g + torch.gather(g_dense.float(), 1, idx.long())
-        return mk.cbsr_scatter_dense(g.contiguous(), idx, ctx.D), None
+        gv = None if g_vals is None else g_vals.float().contiguous()
+        gd = None if g_dense is None else g_dense.float().contiguous()
+        return mk.topk_backward(gv, gd, idx, ctx.D), None
 
 
 def maxk(x: torch.Tensor, k: int):

@@ -61,7 +61,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, V, D, k, seed, use_div, q):
+def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -76,7 +76,7 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q):
 
         shard = maxk_dist.ShardedMaxK(torch.from_numpy(row_ptr), torch.from_numpy(col),
                                       torch.from_numpy(val), rank, world,
-                                      kernels=OracleKernels())
+                                      kernels=OracleKernels(), bounds=bounds)
         v0, v1 = shard.v0, shard.v1
         div = torch.from_numpy(deg[v0:v1]) if use_div else None
         val_l = torch.from_numpy(tv[v0:v1]).requires_grad_(True)
@@ -90,11 +90,11 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q):
         raise
 
 
-def _run(world, V=400, D=64, k=8, seed=0, use_div=True):
+def _run(world, V=400, D=64, k=8, seed=0, use_div=True, bounds=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, V, D, k, seed, use_div, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, V, D, k, seed, use_div, q, bounds))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -118,10 +118,13 @@ def _single(V, D, k, seed, use_div):
     return y, gs
 
 
-@pytest.mark.parametrize("world,use_div", [(2, True), (3, False)])
-def test_sharded_matches_single_process(world, use_div):
+@pytest.mark.parametrize("world,use_div,bounds", [(2, True, None), (3, False, None),
+                                                  (3, True, [0, 150, 150, 400])])
+def test_sharded_matches_single_process(world, use_div, bounds):
+    """The last case gives rank 1 no rows: it still joins both collectives with an all-padding
+    chunk, and the other ranks' results are unchanged."""
     V, D, k, seed = 400, 64, 8, 7
-    outs = _run(world, V, D, k, seed, use_div)
+    outs = _run(world, V, D, k, seed, use_div, bounds)
     y_ref, gs_ref = _single(V, D, k, seed, use_div)
     covered = 0
     for rank, v0, v1, y, gs, bounds in outs:

@@ -243,6 +243,28 @@ def test_empty_graph_and_empty_rows(mk, cuda):
             close(gs, go)
 
 
+def test_zero_rows(mk, cuda):
+    """A shard that owns no rows (maxk_dist with more ranks than hub-balanced ranges): the
+    forward returns [0, D]; the backward still returns the full [num_cols, k] gradient, all
+    zero, in both modes."""
+    D, k, ncols = 64, 16, 50
+    rng = np.random.default_rng(3)
+    cv = torch.from_numpy(rng.random((ncols, k), dtype=np.float32)).to(cuda)
+    ci = torch.from_numpy(np.stack([rng.choice(D, k, replace=False) for _ in range(ncols)])
+                          .astype(np.uint8)).to(cuda)
+    row_ptr = torch.zeros(1, dtype=torch.int32, device=cuda)
+    col = torch.zeros(0, dtype=torch.int32, device=cuda)
+    val = torch.zeros(0, dtype=torch.float32, device=cuda)
+    y = mk.spgemm_forward(row_ptr, col, val, cv, ci, D)
+    assert y.shape == (0, D)
+    g = torch.zeros(0, D, device=cuda)
+    for mode in ("csc", "atomic"):
+        gs = torch.full((ncols, k), 7.0, device=cuda)
+        mk.sspmm_backward(row_ptr, col, val, g, ci, out=gs, mode=mode)
+        torch.cuda.synchronize()
+        assert gs.shape == (ncols, k) and not gs.cpu().numpy().any(), mode
+
+
 def test_output_fully_overwritten(mk, cuda):
     """No zero-init contract: pre-filled output buffers must be overwritten everywhere."""
     rng = np.random.default_rng(5)
@@ -314,6 +336,39 @@ def test_scatter_dense_and_selector_gen(mk, cuda):
     s = sel.cpu().numpy().astype(np.int64)
     assert s.shape == (1000, 32)
     assert all(len(set(r)) == 32 for r in s)
+
+
+@pytest.mark.parametrize("D,k", [(256, 16), (256, 1), (100, 32), (7, 7)])
+def test_fused_maxk_forward_backward(mk, cuda, D, k):
+    """maxk_topk_cbsr_dense == (topk, scatter) and maxk_topk_backward == scatter(gv + gd[sel]),
+    bit-exact (one fp32 add per output), ties (quantised values) and a NaN included."""
+    rng = np.random.default_rng(D + k)
+    V = 700
+    x = np.round(rng.standard_normal((V, D)) * 4).astype(np.float32) / 4  # many ties
+    x[3, D // 2] = np.nan
+    dense, v, i = mk.topk_cbsr_dense(T(x, cuda), k)
+    cv, ci = O.topk(x, k)
+    assert np.array_equal(i.cpu().numpy(), ci)
+    assert np.array_equal(v.cpu().numpy(), cv, equal_nan=True)
+    assert np.array_equal(dense.cpu().numpy(), O.scatter_dense(cv, ci, D), equal_nan=True)
+    # a strided input (ld_x > D) gives the same result
+    wide = np.zeros((V, D + 5), np.float32)
+    wide[:, :D] = x
+    d2, v2, i2 = mk.topk_cbsr_dense(T(wide, cuda)[:, :D], k)
+    assert torch.equal(i2, i) and torch.equal(d2.nan_to_num(), dense.nan_to_num())
+
+    gv = rng.standard_normal((V, k)).astype(np.float32)
+    gd = rng.standard_normal((V, D)).astype(np.float32)
+    picked = np.take_along_axis(gd, ci.astype(np.int64), 1)
+    for a, b, want in ((gv, None, gv), (None, gd, picked), (gv, gd, gv + picked)):
+        got = mk.topk_backward(None if a is None else T(a, cuda),
+                               None if b is None else T(b, cuda), i, D)
+        assert np.array_equal(got.cpu().numpy(), O.scatter_dense(want, ci, D))
+    gd_t = T(gd, cuda)  # in place: grad_x aliases grad_dense
+    mk.topk_backward(T(gv, cuda), gd_t, i, D, out=gd_t)
+    assert np.array_equal(gd_t.cpu().numpy(), O.scatter_dense(gv + picked, ci, D))
+    with pytest.raises(RuntimeError):
+        mk.topk_backward(T(gv, cuda), None, i, D + 1, out=torch.empty(V, D, device=cuda))
 
 
 def test_rocsparse_baseline_matches_oracle(mk, cuda):
