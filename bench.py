@@ -176,6 +176,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # MAXK_BENCH_STACKS=S: every rank logs its stages and dumps all thread stacks to stderr
+    # after S seconds (diagnosing a multi-rank run that stops making progress)
+    stacks_after = float(os.environ.get("MAXK_BENCH_STACKS", "0"))
+    if stacks_after > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(stacks_after, exit=False)
+
+    def stage(msg):
+        if stacks_after > 0 or rank == 0:
+            log(f"[bench] rank {rank}: {msg}")
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # MAXK_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices, collectives
@@ -221,6 +231,7 @@ def main():
         log(f"[bench] graph {args.graph}: V={V} E={E} max_deg={int(deg.max())} "
             f"avg_deg={E / V:.1f} gen {time.time() - t0:.1f}s")
 
+    stage("graph and features ready")
     # ---- shard by vertex range, balanced by nnz (maxk_dist: the module the gloo tests cover)
     if world > 1:
         import maxk_dist
@@ -240,17 +251,15 @@ def main():
     ci_loc = torch.zeros(vmax, k, dtype=torch.uint8, device=dev)
     cv_loc[:nl], ci_loc[:nl] = mk.topk_cbsr(l_X, k)
     if world > 1:
-        cv_all = torch.empty(n_cols, k, device=dev)
-        ci_all = torch.empty(n_cols, k, dtype=torch.uint8, device=dev)
+        # one all-gather of values + selectors per step (ShardedMaxK.gather_cbsr)
+        cv_all, ci_all = shard.gather_cbsr(cv_loc[:nl], ci_loc[:nl])
         gs_all = torch.empty(n_cols, k, device=dev)
         gs_loc = torch.empty(vmax, k, device=dev)
     else:
         cv_all, ci_all = cv_loc, ci_loc
         gs_all = gs_loc = torch.empty(V, k, device=dev)
     y = torch.empty(nl, D, device=dev)
-    if world > 1:
-        maxk_dist.all_gather_rows(cv_all, cv_loc)
-        maxk_dist.all_gather_rows(ci_all, ci_loc)
+    stage(f"shard rows [{v0}, {v1}) edges {El}; CBSR gathered")
     # one validated call (row_ptr/col_idx/selector ranges) before the raw timed launches
     mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, validate=True)
     # per-graph setup (like the reference's warp4 files): transpose plan for the backward
@@ -264,9 +273,9 @@ def main():
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
     def step(ev=None):
+        nonlocal cv_all, ci_all
         if world > 1:
-            maxk_dist.all_gather_rows(cv_all, cv_loc)
-            maxk_dist.all_gather_rows(ci_all, ci_loc)
+            cv_all, ci_all = shard.gather_cbsr(cv_loc[:nl], ci_loc[:nl])
         if ev:
             ev[0].record()
         mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, chunk=args.chunk,
@@ -280,9 +289,11 @@ def main():
         if world > 1:
             maxk_dist.reduce_scatter_rows(gs_loc, gs_all)
 
+    stage(f"transpose plan {t_plan:.3f}s")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    stage("warmup done")
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -294,6 +305,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    stage(f"timed steps done ({elapsed:.3f}s)")
     if dist:
         t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -323,6 +335,7 @@ def main():
         dist.all_reduce(errs, op=dist.ReduceOp.MAX)
         dist_err = [float(errs[0]), float(errs[1])]
         del y_f, gs_f, cv_f, ci_f
+        stage("unsharded self-check done")
 
     fwd_ms = [e[0].elapsed_time(e[1]) for e in evs]
     bwd_ms = [e[1].elapsed_time(e[2]) for e in evs]
@@ -414,6 +427,9 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+    if stacks_after > 0:
+        import faulthandler
+        faulthandler.cancel_dump_traceback_later()
 
 
 if __name__ == "__main__":

@@ -119,6 +119,7 @@ def _single(V, D, k, seed, use_div):
 
 
 @pytest.mark.parametrize("world,use_div,bounds", [(2, True, None), (3, False, None),
+                                                  (4, True, None),
                                                   (3, True, [0, 150, 150, 400])])
 def test_sharded_matches_single_process(world, use_div, bounds):
     """The last case gives rank 1 no rows: it still joins both collectives with an all-padding
