@@ -114,6 +114,19 @@ __device__ __forceinline__ int xcd_contiguous_block(int b, int grid) {
     return (b % kXcds) * per + b / kXcds;
 }
 
+// Raw buffer descriptor over [p, p + bytes), built from wave-uniform values (SGPRs).
+// The range check covers voffset + the instruction offset (not soffset): a load past
+// the end returns 0 and a store past it is dropped, so clamps and predicates on the
+// tail of a segment are unnecessary.  Offsets are 32-bit: no 64-bit address math.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_buffer(const void *p, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo),
+                                             0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                             0x00020000);
+}
+
 // Orders this wave's LDS traffic at a phase change (all lanes of ONE wave):
 // LDS executes a wave's instructions in order; this only stops the compiler
 // from moving LDS accesses across the boundary.

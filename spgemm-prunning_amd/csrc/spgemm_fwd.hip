@@ -113,47 +113,90 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack_kernel(const float *__re
     }
 }
 
-template <int KG, int U>
+template <int KG, int U, bool WIDE>
 struct EdgeWalker {
     static constexpr int G = kWave / KG;  // edges per wave step
 
     // acc_g[sel] += val[e] * value over e in [sb, se), sb < se.  acc_g is this
-    // lane's group copy.  Out-of-range edges/lanes load a clamped (valid)
-    // address and add 0, so hipcc keeps all U gathers in flight.
-    // Padding lanes (l >= k) write to the trash column: two lanes of one group
-    // must never hit the same live address in one ds_write.
+    // lane's group copy.  Padding lanes (l >= k) and edges past se write to the trash
+    // column: two lanes of one group must never hit the same live address in one
+    // ds_write, and an idle lane's product (weight 0 times any value) must not reach a
+    // live column.
+    // Default: every load goes through a wave-uniform buffer descriptor with 32-bit
+    // offsets (wave_buffer, common.h): col_idx / edge_val over [sb, se) (past se they
+    // return 0: column 0, weight 0, so nothing is clamped), the record table at
+    // c*RS + 4l (values) and c*RS + 4k + 2l (selectors), one 24-bit multiply-add each.
+    // WIDE (tables past 2^24 columns or 4 GiB): 64-bit addresses, clamped loads.
     __device__ __forceinline__ static void run(float *acc_g, const int32_t *__restrict__ col_idx,
                                                const float *__restrict__ edge_val,
                                                const uint8_t *__restrict__ rec, int RS, int sb,
                                                int se, int k, int trash, int lane) {
         const int grp = lane / KG;
         const int l0 = lane % KG;
-        const int last = se - 1;
-        for (int base = sb; base < se; base += G * U) {
-            int c[U];
-            float w[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = base + u * G + grp;
-                const int ec = e < se ? e : last;
-                c[u] = col_idx[ec];
-                const float wv = edge_val[ec];
-                w[u] = e < se ? wv : 0.f;
-            }
-            for (int lb = 0; lb < k; lb += KG) {  // one pass unless k > 64
-                const int l = lb + l0;
-                const bool lok = l < k;
-                const int lc = lok ? l : k - 1;
-                float v[U];
-                int s[U];
+        if constexpr (!WIDE) {
+            const int n = se - sb;  // wave-uniform, <= chunk
+            const auto crs = wave_buffer(col_idx + sb, (uint32_t)n * 4u);
+            const auto vrs = wave_buffer(edge_val + sb, (uint32_t)n * 4u);
+            const auto rrs = wave_buffer(rec, 0xffffffffu);  // offsets < num_cols * RS < 2^32
+            for (int base = 0; base < n; base += G * U) {
+                int c[U];
+                float w[U];
+                const int lo = (base + grp) * 4;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    const uint8_t *p = rec + (size_t)(uint32_t)c[u] * RS;
-                    v[u] = reinterpret_cast<const float *>(p)[lc];
-                    s[u] = reinterpret_cast<const uint16_t *>(p + 4 * k)[lc];
+                    c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+                    w[u] = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
                 }
+                for (int lb = 0; lb < k; lb += KG) {  // one pass unless k > 64
+                    const int l = lb + l0;
+                    const bool lok = l < k;
+                    const uint32_t lc = (uint32_t)(lok ? l : k - 1);
+                    const uint32_t vo = 4u * lc, so = 4u * (uint32_t)k + 2u * lc;
+                    float v[U];
+                    int s[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) acc_g[lok ? s[u] : trash] += w[u] * v[u];
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t ro = __umul24((uint32_t)c[u], (uint32_t)RS);
+                        v[u] = __uint_as_float(
+                            __builtin_amdgcn_raw_buffer_load_b32(rrs, (int)(ro + vo), 0, 0));
+                        s[u] = __builtin_amdgcn_raw_buffer_load_b16(rrs, (int)(ro + so), 0, 0);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const bool live = lok && base + u * G + grp < n;
+                        acc_g[live ? s[u] : trash] += w[u] * v[u];
+                    }
+                }
+            }
+        } else {
+            const int last = se - 1;
+            for (int base = sb; base < se; base += G * U) {
+                int c[U];
+                float w[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int e = base + u * G + grp;
+                    const int ec = e < se ? e : last;
+                    c[u] = col_idx[ec];
+                    const float wv = edge_val[ec];
+                    w[u] = e < se ? wv : 0.f;
+                }
+                for (int lb = 0; lb < k; lb += KG) {
+                    const int l = lb + l0;
+                    const bool lok = l < k;
+                    const int lc = lok ? l : k - 1;
+                    float v[U];
+                    int s[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint8_t *p = rec + (size_t)(uint32_t)c[u] * RS;
+                        v[u] = reinterpret_cast<const float *>(p)[lc];
+                        s[u] = reinterpret_cast<const uint16_t *>(p + 4 * k)[lc];
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) acc_g[lok ? s[u] : trash] += w[u] * v[u];
+                }
             }
         }
     }
@@ -200,7 +243,7 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
     wave_lds_fence();
 }
 
-template <int KG, int U>
+template <int KG, int U, bool WIDE>
 __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
     const float *__restrict__ edge_val, const uint8_t *__restrict__ rec, int RS,
@@ -231,7 +274,7 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
         if (d1 - r < se) se = d1 - r;
         if (sb < se) {
             wave_lds_fence();
-            EdgeWalker<KG, U>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se, k, DS - 1,
+            EdgeWalker<KG, U, WIDE>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se, k, DS - 1,
                                    lane);
             const float div = row_div ? row_div[r - 1] : 1.f;
             flush_row<NC>(acc, DS, slab + (int64_t)item * D, D, div, row_div != nullptr, lane);
@@ -248,7 +291,7 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
         if (d1 - r - 1 < se) se = d1 - r - 1;
         wave_lds_fence();
         if (rb < se)
-            EdgeWalker<KG, U>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se, k, DS - 1,
+            EdgeWalker<KG, U, WIDE>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se, k, DS - 1,
                                    lane);
         const float div = row_div ? row_div[r] : 1.f;
         flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane);
@@ -299,9 +342,16 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
     constexpr int NC = kWave / KG;
     const size_t lds = (size_t)kWavesPerBlock * NC * L.DS * sizeof(float);
     const dim3 grid((unsigned)ceil_div(L.n_items, kWavesPerBlock));
-    hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U>), grid, dim3(kBlock), lds, s, row_ptr, col_idx,
-                       edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows, num_e, D,
-                       L.DS, k, L.chunk, L.n_items);
+    // 32-bit record offsets need c < 2^24 (24-bit multiply) and the table under 4 GiB
+    const int64_t num_cols = (int64_t)(L.rec_bytes / L.RS);
+    if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32))
+        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false>), grid, dim3(kBlock), lds, s, row_ptr,
+                           col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows,
+                           num_e, D, L.DS, k, L.chunk, L.n_items);
+    else
+        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, true>), grid, dim3(kBlock), lds, s, row_ptr,
+                           col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows,
+                           num_e, D, L.DS, k, L.chunk, L.n_items);
 }
 
 }  // namespace

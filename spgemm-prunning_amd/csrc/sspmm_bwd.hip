@@ -25,83 +25,91 @@
 namespace maxk {
 namespace {
 
-enum { kAtomic = 0, kStore = 1, kStoreX4 = 2 };
+enum { kAtomic = 0, kStore = 1, kStoreX4 = 2, kStoreX4W = 3 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // kStoreX4 (k % 4 == 0): LR = pow2ceil(k/4) lanes per edge, each lane owning 4
 // consecutive l: one u32 selector load, four LDS reads, one 16-B store; 64/LR
 // edges per wave step (4x fewer memory instructions per edge than one l per
-// lane).  T rows [sb, se) are addressed through a wave-uniform buffer
-// descriptor; a masked lane's offset lies past its end and the hardware drops
-// the store, so no store is predicated and no dummy row is touched.  Cache
-// policy of the T stores: MAXK_T_AUX (0 plain, 2 nt, 16 sc1).  Store lag as in
+// lane).  All memory goes through wave-uniform buffer descriptors with 32-bit
+// offsets (wave_buffer, common.h), which keeps 64-bit address math out of the loop:
+//  * col_idx / edge_val over the segment [sb, se): the lane's offset is fixed per
+//    batch and the step's part is the instruction's immediate; past se the loads
+//    return 0 (column 0, weight 0), so nothing is clamped;
+//  * the selector table: offset c*k + 4q, one 24-bit multiply-add (kStoreX4W, for
+//    tables past 2^24 columns, a 32-bit multiply);
+//  * T rows [sb, se): past se, or for lanes q >= k/4 (offset pushed past 2^31), the
+//    hardware drops the store, so no store is predicated.
+// Cache policy of the T stores: MAXK_T_AUX (0 plain, 2 nt, 16 sc1).  Store lag as in
 // push_edges below.
-template <int LR, int U>
+template <int LR, int U, bool WIDE>
 __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__restrict__ col_idx,
                                         const float *__restrict__ edge_val,
                                         const uint8_t *__restrict__ cbsr_idx,
                                         float *__restrict__ T, int sb, int se, int k, int lane) {
     constexpr int G = kWave / LR;
     constexpr int GU = G * U;
-    constexpr uint32_t kDrop = 0x80000000u;
     const int grp = lane / LR;
     const int q = lane % LR;
     const int k4 = k >> 2;
-    const bool qok = q < k4;
-    const int qc = qok ? q : k4 - 1;
-    const int last = se - 1;
-    const uint64_t tb = reinterpret_cast<uint64_t>(T + (size_t)(uint32_t)sb * k);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)tb);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32));
-    const int nbytes = __builtin_amdgcn_readfirstlane((se - sb) * k * 4);  // <= 2 MiB per segment
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void *>(((uint64_t)hi << 32) | lo), 0, nbytes, 0x00020000);
-    const uint8_t *sel = cbsr_idx + 4 * qc;
+    const int n = se - sb;  // wave-uniform, <= chunk
+    const auto crs = wave_buffer(col_idx + sb, (uint32_t)n * 4u);
+    const auto vrs = wave_buffer(edge_val + sb, (uint32_t)n * 4u);
+    const auto srs = wave_buffer(cbsr_idx, 0xffffffffu);  // offsets < num_cols*k < 2^31
+    const auto trs = wave_buffer(T + (size_t)(uint32_t)sb * k, (uint32_t)n * k * 4u);  // <= 2 MiB
+    const uint32_t qsel = 4u * (uint32_t)(q < k4 ? q : k4 - 1);
+    const uint32_t qst = q < k4 ? 16u * q : 0x80000000u;  // store offset term; past the end if idle
+    const uint32_t kb = 4u * (uint32_t)k;                    // T row bytes
+    auto sel_off = [&](int c) -> int {
+        return WIDE ? (int)((uint32_t)c * (uint32_t)k + qsel)
+                    : (int)(__umul24((uint32_t)c, (uint32_t)k) + qsel);
+    };
     int c[U];
     float w[U];
+    {
+        const int lo = grp * 4;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int e = sb + u * G + grp;
-        const int ec = e < se ? e : last;
-        c[u] = col_idx[ec];
-        w[u] = edge_val[ec];
+        for (int u = 0; u < U; ++u) {
+            c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+            w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
+        }
     }
     u32x4 xp[U];
-    uint32_t op[U];
+    uint32_t sto = 0;  // T byte offset of the pending batch's step 0 for this lane
     bool pending = false;
-    for (int base = sb;; base += GU) {
-        const bool has_next = base + GU < se;  // wave-uniform
+    for (int base = 0;; base += GU) {  // base: edge offset inside the segment
+        const bool has_next = base + GU < n;  // wave-uniform
         int cn[U];
         float wn[U];
         if (has_next) {
+            const int lo = (base + GU + grp) * 4;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int e = base + GU + u * G + grp;
-                const int ec = e < se ? e : last;
-                cn[u] = col_idx[ec];
-                wn[u] = edge_val[ec];
+                cn[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+                wn[u] = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
             }
         }
         uint32_t sv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            sv[u] = *reinterpret_cast<const uint32_t *>(sel + (size_t)(uint32_t)c[u] * k);
+            sv[u] = __builtin_amdgcn_raw_buffer_load_b32(srs, sel_off(c[u]), 0, 0);
         if (pending) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                __builtin_amdgcn_raw_buffer_store_b128(xp[u], rsrc, (int)op[u], 0, MAXK_T_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0,
+                                                       MAXK_T_AUX);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int e = base + u * G + grp;
             const uint32_t s = sv[u];
             xp[u].x = __float_as_uint(w[u] * g_lds[s & 255u]);
             xp[u].y = __float_as_uint(w[u] * g_lds[(s >> 8) & 255u]);
             xp[u].z = __float_as_uint(w[u] * g_lds[(s >> 16) & 255u]);
             xp[u].w = __float_as_uint(w[u] * g_lds[s >> 24]);
-            op[u] = (e < se && qok) ? (uint32_t)((e - sb) * k + 4 * q) * 4u : kDrop;
         }
+        sto = (uint32_t)(base + grp) * kb + qst;
         pending = true;
         if (!has_next) break;
 #pragma unroll
@@ -112,7 +120,7 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        __builtin_amdgcn_raw_buffer_store_b128(xp[u], rsrc, (int)op[u], 0, MAXK_T_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0, MAXK_T_AUX);
 }
 
 // Walk edges [sb, se) (sb < se) of one staged row.  All loads are
@@ -131,8 +139,8 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
                                            const uint8_t *__restrict__ cbsr_idx,
                                            float *__restrict__ dst, int dummy, int sb, int se,
                                            int k, int lane) {
-    if constexpr (MODE == kStoreX4) {
-        push_x4<KG, U>(g_lds, col_idx, edge_val, cbsr_idx, dst, sb, se, k, lane);
+    if constexpr (MODE == kStoreX4 || MODE == kStoreX4W) {
+        push_x4<KG, U, MODE == kStoreX4W>(g_lds, col_idx, edge_val, cbsr_idx, dst, sb, se, k, lane);
         return;
     }
     constexpr int G = kWave / KG;
@@ -424,17 +432,22 @@ int pick_depth(int64_t num_e, int64_t rows, int per_step, int lo, int hi) {
 template <int MODE>
 int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 const float *edge_val, const float *grad, const float *row_div,
-                const uint8_t *cbsr_idx, float *dst, int nr, int64_t num_e, int D, int k,
-                int chunk) {
+                const uint8_t *cbsr_idx, float *dst, int nr, int64_t num_cols, int64_t num_e,
+                int D, int k, int chunk) {
     const int n_items = n_items_for(nr, num_e, chunk);
     const dim3 grid((unsigned)ceil_div(n_items, kWavesPerBlock));
     if (MODE == kStore && MAXK_BWD_X4 && k % 4 == 0) {
         const int lr = lanes_per_edge(k / 4);
         const int u = MAXK_X4_U > 0 ? MAXK_X4_U : pick_depth(num_e, nr, kWave / lr, 4, 16);
+        const bool wide = num_cols >= (1 << 24);  // selector offsets need a 32-bit multiply
         switch (lr) {
 #define MAXK_CASE(LRV)                                                                       \
     case LRV:                                                                                \
-        if (u <= 4)                                                                          \
+        if (wide)                                                                            \
+            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 8, kStoreX4W>), grid, dim3(kBlock), 0, \
+                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
+                               nr, num_e, D, k, chunk, n_items);                             \
+        else if (u <= 4)                                                                     \
             hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 4, kStoreX4>), grid, dim3(kBlock), 0,  \
                                s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
                                nr, num_e, D, k, chunk, n_items);                             \
@@ -549,7 +562,7 @@ extern "C" int maxk_sspmm_backward(const int32_t *row_ptr, const int32_t *col_id
                  "CSR/grad/selector pointers must not be NULL");
     MAXK_REQUIRE(num_cols > 0, "edges present but num_cols == 0");
     return launch_push<kAtomic>(s, row_ptr, col_idx, edge_val, grad_out, row_div, cbsr_idx,
-                                grad_cbsr, (int)num_rows, num_e, dim_origin, dim_k,
+                                grad_cbsr, (int)num_rows, num_cols, num_e, dim_origin, dim_k,
                                 bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS));
 }
 
@@ -587,8 +600,9 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
     const int k = dim_k;
     if (num_e > 0 && num_rows > 0) {
         if (int rc = launch_push<kStore>(s, row_ptr, col_idx, edge_val, grad_out, row_div,
-                                         cbsr_idx, T, (int)num_rows, num_e, dim_origin,
-                                         k, bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS)))
+                                         cbsr_idx, T, (int)num_rows, num_cols, num_e,
+                                         dim_origin, k,
+                                         bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS)))
             return rc;
     }
     const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
