@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 OP_KERNELS = {
     "spgemm_forward": ["cbsr_pack_kernel", "spgemm_fwd_kernel", "slab_fixup_kernel<0>"],
     "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>"],
+    "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
 }
 
@@ -167,7 +168,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--bwd-mode", default="csc", choices=["csc", "atomic"])
+    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "bucket", "csc", "atomic"])
     ap.add_argument("--graph-dir", default=None,
                     help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
     ap.add_argument("--no-cpu-spmm", action="store_true")
@@ -262,10 +263,11 @@ def main():
     stage(f"shard rows [{v0}, {v1}) edges {El}; CBSR gathered")
     # one validated call (row_ptr/col_idx/selector ranges) before the raw timed launches
     mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, validate=True)
-    # per-graph setup (like the reference's warp4 files): transpose plan for the backward
+    # per-graph setup (like the reference's warp4 files): the backward's bucket / transpose plan
+    args.bwd_mode = mk._bwd_mode(args.bwd_mode, k, El, n_cols, nl)  # "auto" -> the mode that runs
     torch.cuda.synchronize()
     t_plan = time.perf_counter()
-    plan = mk.transpose_plan(l_col, n_cols) if args.bwd_mode == "csc" else None
+    plan = mk.backward_plan(l_col, n_cols, k, args.bwd_mode)
     torch.cuda.synchronize()
     t_plan = time.perf_counter() - t_plan
 
@@ -289,7 +291,7 @@ def main():
         if world > 1:
             maxk_dist.reduce_scatter_rows(gs_loc, gs_all)
 
-    stage(f"transpose plan {t_plan:.3f}s")
+    stage(f"backward plan ({args.bwd_mode}) {t_plan:.3f}s")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -358,7 +360,7 @@ def main():
         "fwd_gteps": round(El / fwd_avg / 1e6, 3), "bwd_gteps": round(El / bwd_avg / 1e6, 3),
         "fwd_alg_GBs": round(B_f / fwd_avg / 1e6, 1), "bwd_alg_GBs": round(B_b / bwd_avg / 1e6, 1),
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
-        "bwd_mode": args.bwd_mode, "transpose_plan_s": round(t_plan, 4),
+        "bwd_mode": args.bwd_mode, "backward_plan_s": round(t_plan, 4),
     }
     if world > 1:
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],

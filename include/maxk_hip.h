@@ -110,6 +110,43 @@ int maxk_transpose_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
                         size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Same backward, two-phase with a bucketed phase 2 (the default for k % 4 == 0):
+ * phase 1 as in maxk_sspmm_backward_csc; phase 2 gives every bucket of 2^bucket_shift
+ * consecutive destinations one workgroup, which reads the bucket's contribution rows in
+ * CSR order (neighbouring rows share cache lines) and sums them in an fp64 LDS
+ * accumulator.  The fp32 result does not depend on the order of the adds except in rare
+ * rounding ties (fp64 partial sums); use maxk_sspmm_backward_csc where every bit must
+ * repeat.  Needs dim_k % 4 == 0 and 2^bucket_shift * (dim_k + 1) <= 18432, the bucket plan of
+ * the graph built with that shift (maxk_bucket_plan) and a workspace of
+ * maxk_sspmm_backward_bucket_workspace_size(...) bytes (about num_e*k*4).
+ * Replaces the same reference kernels as maxk_sspmm_backward.
+ * ------------------------------------------------------------------------- */
+size_t maxk_sspmm_backward_bucket_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                 int64_t num_e, int32_t dim_origin,
+                                                 int32_t dim_k, int32_t chunk_edges);
+int maxk_sspmm_backward_bucket(const int32_t *row_ptr, const int32_t *col_idx,
+                               const float *edge_val, const float *grad_out, const float *row_div,
+                               const uint8_t *cbsr_idx, const int32_t *bucket_ptr,
+                               const int32_t *bucket_eid, const uint16_t *bucket_dst,
+                               int32_t bucket_shift, float *grad_cbsr, int64_t num_rows,
+                               int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                               int32_t chunk_edges, void *workspace, size_t workspace_bytes,
+                               void *stream);
+
+/* Bucket plan of a CSR graph (once per graph and shift): bucket_ptr[nb+1] with
+ * nb = maxk_bucket_count(num_cols, shift), bucket_eid[num_e] = the CSR edge ids whose
+ * column lies in each bucket (in CSR order), bucket_dst[num_e] = that column minus the
+ * bucket's first column.  maxk_bucket_shift(k) is the largest shift the accumulator
+ * allows for k (-1 for k <= 0).  Like maxk_transpose_plan, the MI355X replacement for the
+ * CSC side files of generate_meta_csc.py:14-93 / load_warp4_metadata_csc. */
+int maxk_bucket_shift(int32_t dim_k);
+int64_t maxk_bucket_count(int64_t num_cols, int32_t bucket_shift);
+size_t maxk_bucket_plan_workspace_size(int64_t num_cols, int64_t num_e);
+int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
+                     int32_t bucket_shift, int32_t *bucket_ptr, int32_t *bucket_eid,
+                     uint16_t *bucket_dst, void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * CBSR encode (MaxK top-k): per row the k largest of dim_origin values, in
  * torch.topk(largest=True, sorted=True) order (value descending; NaN largest;
  * equal values by ascending column).  x has leading dimension ld_x (elements).

@@ -15,6 +15,11 @@ constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kBlock = 256;        // threads per workgroup (4 waves; 512 / 1024 measured slower)
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows are 256 floats
+// Bucketed backward, phase 2: fp64 LDS accumulator of one destination bucket (144 KiB);
+// a bucket holds 2^shift destinations with 2^shift * (k + 1) <= kBucketAccDoubles (rows
+// padded to k + 1 doubles so the rows of one wave instruction's random destinations spread
+// over the LDS banks instead of all starting on the same few).
+constexpr int kBucketAccDoubles = 18432;
 
 // Tuning knobs (compile-time; tools/tune.sh builds variants).  *_U = edge
 // batches in flight per wave, *_WAVES = __launch_bounds__ min waves per SIMD.
@@ -53,6 +58,12 @@ constexpr int kMaxDim = 256;       // uint8 selector range: per-wave LDS rows ar
 #endif
 #ifndef MAXK_PACK_GRID  // grid cap of the grid-stride record pack
 #define MAXK_PACK_GRID 4096
+#endif
+#ifndef MAXK_BUCKET_U  // bucketed phase-2 depth (wave steps of loads in flight)
+#define MAXK_BUCKET_U 8
+#endif
+#ifndef MAXK_BUCKET_PARTS  // bucketed phase 2: parts (workgroups) per CU
+#define MAXK_BUCKET_PARTS 4
 #endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0

@@ -403,6 +403,140 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
     }
 }
 
+// ---- phase 2, bucketed: grad_cbsr[c, :] = sum of T[e, :] over the entries of c's bucket ----
+// The bucket-ordered entry list (bucket_eid: per bucket of 2^shift destinations, the CSR
+// edge ids into it in CSR order) is cut into equal parts of `part` entries, one
+// 1024-thread workgroup each, so a heavy bucket (power-law in-degrees: the largest
+// Reddit-sized bucket holds 1.2x the mean) never sets the kernel time alone.  A part
+// walks the buckets it meets; per bucket it sums into an fp64 LDS accumulator
+// [2^shift, k + 1] and stores the bucket's rows directly when it holds all of the bucket's
+// entries, else one fp32 partial to its slab slot (slot 0: the part's first bucket, 1: its
+// last); bucket_fixup_kernel adds the partials in part order and zero-fills empty buckets.
+// Entries are read in order, LR = pow2ceil(k/4) lanes per T row (16-B loads), 64/LR
+// consecutive entries per wave instruction: neighbouring entries of one source row are
+// neighbouring T rows, so one line request serves several of them (a Reddit-sized bucket
+// of 1024 destinations holds ~2.2 edges of every source row).  Sums go through ds_add_f64:
+// on gfx950 it costs about a ds_write (8.8 cycles per wave instruction), ds_add_f32 costs
+// 193 (tools/lds_atomic_probe.hip).  fp64 partial sums make the fp32 result independent of
+// the order of the adds except in rare rounding ties.  U steps of loads in flight, the
+// next step's entry ids prefetched.
+template <int LR, int U>
+__global__ __launch_bounds__(1024) void bucket_sum_kernel(
+    const float *__restrict__ T, const int32_t *__restrict__ bucket_ptr,
+    const int32_t *__restrict__ bucket_eid, const uint16_t *__restrict__ bucket_dst,
+    float *__restrict__ grad_cbsr, float *__restrict__ slab, int num_cols, int n_buckets,
+    int num_e, int k, int shift, int part) {
+    __shared__ double acc[kBucketAccDoubles];
+    __shared__ int s_j0;
+    constexpr int EPI = kWave / LR;  // entries per wave instruction
+    constexpr int STEP = EPI * U;    // entries per wave step
+    const int tid = threadIdx.x;
+    const int lane = lane_id(), w = tid / kWave;
+    const int g = lane / LR, q = lane % LR;
+    const int kq = k >> 2;
+    const bool qok = q < kq;
+    const int nacc = k << shift;  // floats of one bucket (output / slab slot)
+    const int ks = k + 1;         // LDS row stride (doubles)
+    const int nlds = ks << shift;
+    const int p = blockIdx.x;
+    const int p0 = p * part, p1 = num_e - p0 > part ? p0 + part : num_e;
+    if (tid == 0) {  // first bucket of the part: the last j with bucket_ptr[j] <= p0
+        int lo = 0, hi = n_buckets - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (bucket_ptr[mid] <= p0) lo = mid; else hi = mid - 1;
+        }
+        s_j0 = lo;
+    }
+    __syncthreads();
+    const int j0 = s_j0;
+    const float4 *__restrict__ T4 = reinterpret_cast<const float4 *>(T);
+    for (int j = j0; j < n_buckets; ++j) {
+        const int b0 = bucket_ptr[j], b1 = bucket_ptr[j + 1];
+        if (b0 >= p1) break;
+        if (b0 == b1) continue;  // empty bucket: zero-filled by the fixup
+        const int s0 = b0 > p0 ? b0 : p0, s1 = b1 < p1 ? b1 : p1;
+        for (int i = tid; i < nlds; i += 1024) acc[i] = 0.0;
+        __syncthreads();
+        int base = s0 + w * STEP;
+        int e[U], d[U];
+        auto load_ids = [&](int b) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int t = b + u * EPI + g;
+                const int tc = t < s1 ? t : s1 - 1;
+                e[u] = bucket_eid[tc];
+                d[u] = t < s1 ? (int)bucket_dst[tc] : -1;
+            }
+        };
+        if (base < s1) load_ids(base);
+        for (; base < s1; base += 16 * STEP) {
+            float4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                v[u] = T4[(size_t)(uint32_t)e[u] * (uint32_t)kq + (qok ? q : 0)];
+            int dc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) dc[u] = d[u];
+            if (base + 16 * STEP < s1) load_ids(base + 16 * STEP);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (dc[u] >= 0 && qok) {
+                    double *a = &acc[dc[u] * ks + 4 * q];
+                    atomicAdd(a + 0, (double)v[u].x);
+                    atomicAdd(a + 1, (double)v[u].y);
+                    atomicAdd(a + 2, (double)v[u].z);
+                    atomicAdd(a + 3, (double)v[u].w);
+                }
+            }
+        }
+        __syncthreads();
+        const int64_t c0 = (int64_t)j << shift;
+        const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
+        const bool whole = b0 >= p0 && b1 <= p1;
+        float *o = whole ? grad_cbsr + c0 * k
+                         : slab + ((size_t)p * 2 + (j == j0 ? 0 : 1)) * (size_t)nacc;
+        for (int i = tid; i < rows * k; i += 1024) {
+            const int r = i / k;
+            o[i] = (float)acc[i + r];  // row r starts at r * (k + 1)
+        }
+        __syncthreads();
+    }
+}
+
+// Buckets no single part holds whole: the sum of their parts' slab partials in part order;
+// empty buckets: zeros.  One thread per 4 floats; blockIdx.x = bucket, blockIdx.y = tile.
+__global__ __launch_bounds__(kBlock) void bucket_fixup_kernel(
+    const int32_t *__restrict__ bucket_ptr, const float *__restrict__ slab,
+    float *__restrict__ grad_cbsr, int num_cols, int k, int shift, int part) {
+    const int j = blockIdx.x;
+    const int b0 = bucket_ptr[j], b1 = bucket_ptr[j + 1];
+    const int plo = b0 / part, phi = b1 > 0 ? (b1 - 1) / part : 0;
+    if (b0 != b1 && plo == phi) return;  // stored whole by its part
+    const int64_t c0 = (int64_t)j << shift;
+    const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
+    const int n4 = rows * k / 4;  // k % 4 == 0
+    const int i = blockIdx.y * kBlock + threadIdx.x;
+    if (i >= n4) return;
+    float4 *o = reinterpret_cast<float4 *>(grad_cbsr + c0 * k) + i;
+    if (b0 == b1) {
+        *o = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    const size_t nacc4 = ((size_t)k << shift) / 4;
+    const float4 *sl = reinterpret_cast<const float4 *>(slab);
+    const int lo_slot = plo * part < b0 ? 1 : 0;  // bucket j is the last bucket of part plo
+    float4 a = sl[((size_t)plo * 2 + lo_slot) * nacc4 + i];
+    for (int p = plo + 1; p <= phi; ++p) {
+        const float4 b = sl[(size_t)p * 2 * nacc4 + i];
+        a.x += b.x;
+        a.y += b.y;
+        a.z += b.z;
+        a.w += b.w;
+    }
+    *o = a;
+}
+
 // Auto item size: ~`per_slot` items per resident wave slot on 256 CUs, in [256, 2048].
 int bwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int per_slot) {
     if (chunk > 0) return chunk;
@@ -645,4 +779,92 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
     }
     MAXK_LAUNCHED("csc_sum_kernel");
     return launch_slab_fixup<1>(slab, slab_row, grad_cbsr, k, L.n_items, s);
+}
+
+// Bucketed phase 2: entries per part (~MAXK_BUCKET_PARTS parts per CU, at least 16384).
+int bucket_part(int64_t num_e) {
+    int64_t p = ceil_div(num_e, 256LL * MAXK_BUCKET_PARTS);
+    return (int)(p < 16384 ? 16384 : p);
+}
+
+extern "C" size_t maxk_sspmm_backward_bucket_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                            int64_t num_e, int32_t dim_origin,
+                                                            int32_t dim_k, int32_t chunk_edges) {
+    (void)num_rows; (void)num_cols; (void)dim_origin; (void)chunk_edges;
+    if (num_e < 0 || dim_k <= 0) return 0;
+    const int shift = maxk_bucket_shift(dim_k);
+    const size_t t = ((size_t)(num_e + 1) * dim_k * sizeof(float) + 255) & ~(size_t)255;
+    const size_t parts = (size_t)ceil_div(num_e, bucket_part(num_e));
+    return t + parts * 2 * ((size_t)dim_k << shift) * sizeof(float);
+}
+
+extern "C" int maxk_sspmm_backward_bucket(const int32_t *row_ptr, const int32_t *col_idx,
+                                          const float *edge_val, const float *grad_out,
+                                          const float *row_div, const uint8_t *cbsr_idx,
+                                          const int32_t *bucket_ptr, const int32_t *bucket_eid,
+                                          const uint16_t *bucket_dst, int32_t bucket_shift,
+                                          float *grad_cbsr, int64_t num_rows, int64_t num_cols,
+                                          int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                                          int32_t chunk_edges, void *workspace,
+                                          size_t workspace_bytes, void *stream) {
+    clear_error();
+    if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges)) return rc;
+    MAXK_REQUIRE(dim_k % 4 == 0, "bucketed backward needs dim_k %% 4 == 0, got %d", dim_k);
+    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 16 &&
+                     ((int64_t)(dim_k + 1) << bucket_shift) <= kBucketAccDoubles,
+                 "bucket_shift %d too large for dim_k %d (2^shift * (k + 1) <= %d)", bucket_shift,
+                 dim_k, kBucketAccDoubles);
+    hipStream_t s = as_stream(stream);
+    if (num_cols == 0) return MAXK_OK;
+    MAXK_REQUIRE(grad_cbsr && bucket_ptr, "grad_cbsr/bucket_ptr must not be NULL");
+    MAXK_REQUIRE(num_e == 0 || (row_ptr && col_idx && edge_val && grad_out && cbsr_idx &&
+                                bucket_eid && bucket_dst),
+                 "CSR/grad/selector/bucket pointers must not be NULL");
+    const size_t need = maxk_sspmm_backward_bucket_workspace_size(num_rows, num_cols, num_e,
+                                                                  dim_origin, dim_k, chunk_edges);
+    MAXK_REQUIRE(workspace && workspace_bytes >= need,
+                 "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
+    float *T = reinterpret_cast<float *>(workspace);
+    const int k = dim_k;
+    if (num_e > 0 && num_rows > 0) {
+        if (int rc = launch_push<kStore>(s, row_ptr, col_idx, edge_val, grad_out, row_div,
+                                         cbsr_idx, T, (int)num_rows, num_cols, num_e,
+                                         dim_origin, k,
+                                         bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS)))
+            return rc;
+    }
+    const int64_t nb = (num_cols + (1LL << bucket_shift) - 1) >> bucket_shift;
+    const int part = bucket_part(num_e);
+    const int64_t parts = ceil_div(num_e, part);
+    float *slab = reinterpret_cast<float *>(
+        reinterpret_cast<char *>(workspace) +
+        (((size_t)(num_e + 1) * dim_k * sizeof(float) + 255) & ~(size_t)255));
+    const int nc = (int)num_cols, ne = (int)num_e, nbi = (int)nb;
+    switch (parts > 0 ? lanes_per_edge(k / 4) : 0) {
+        case 0:
+            break;
+#define MAXK_CASE(LRV)                                                                          \
+    case LRV:                                                                                   \
+        hipLaunchKernelGGL((bucket_sum_kernel<LRV, MAXK_BUCKET_U>), dim3((unsigned)parts),      \
+                           dim3(1024), 0, s, T, bucket_ptr, bucket_eid, bucket_dst, grad_cbsr,  \
+                           slab, nc, nbi, ne, k, bucket_shift, part);                           \
+        break;
+        MAXK_CASE(1)
+        MAXK_CASE(2)
+        MAXK_CASE(4)
+        MAXK_CASE(8)
+        MAXK_CASE(16)
+        MAXK_CASE(32)
+        MAXK_CASE(64)
+#undef MAXK_CASE
+        default:
+            set_error("unsupported lane group");
+            return MAXK_ERR_INVALID;
+    }
+    MAXK_LAUNCHED("bucket_sum_kernel");
+    hipLaunchKernelGGL(bucket_fixup_kernel,
+                       dim3((unsigned)nb, (unsigned)ceil_div(((int64_t)k << bucket_shift) / 4, kBlock)),
+                       dim3(kBlock), 0, s, bucket_ptr, slab, grad_cbsr, nc, k, bucket_shift, part);
+    MAXK_LAUNCHED("bucket_fixup_kernel");
+    return MAXK_OK;
 }

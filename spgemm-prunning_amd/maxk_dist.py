@@ -82,8 +82,8 @@ class _HipKernels:
         return self.mk.sspmm_backward(indptr, indices, values, grad, cbsr_idx, row_div=row_div,
                                       plan=plan)
 
-    def transpose_plan(self, indices, num_cols):
-        return self.mk.transpose_plan(indices, num_cols)
+    def backward_plan(self, indices, num_cols, k, num_rows=None):
+        return self.mk.backward_plan(indices, num_cols, k, num_rows=num_rows)
 
 
 class ShardedMaxK:
@@ -110,7 +110,7 @@ class ShardedMaxK:
         owner = torch.searchsorted(starts[1:], cols, right=True)
         self.col_idx = (owner * self.vmax + (cols - starts[owner])).to(torch.int32).contiguous()
         self.values = values[e0:e1].to(self.device, torch.float32).contiguous()
-        self._plan = None
+        self._plans = {}
 
     # ---- helpers
     def gather_cbsr(self, val_local: torch.Tensor, idx_local: torch.Tensor):
@@ -133,10 +133,14 @@ class ShardedMaxK:
         idx_all = recv[:, vb:].contiguous().view(idx_local.dtype).view(self.n_cols, k)
         return val_all, idx_all
 
-    def plan(self):
-        if self._plan is None and hasattr(self.kernels, "transpose_plan"):
-            self._plan = self.kernels.transpose_plan(self.col_idx, self.n_cols)
-        return self._plan
+    def plan(self, k: int):
+        """The backward's per-graph plan at width k (built once per k; None for a kernel
+        backend without plans, e.g. the CPU oracle in the tests)."""
+        if k not in self._plans:
+            bp = getattr(self.kernels, "backward_plan", None)
+            self._plans[k] = (bp(self.col_idx, self.n_cols, k, num_rows=self.n_local)
+                              if bp is not None else None)
+        return self._plans[k]
 
     # ---- the two aggregation passes
     def forward(self, val_all, idx_all, D: int, row_div_local=None) -> torch.Tensor:
@@ -149,7 +153,8 @@ class ShardedMaxK:
         """CBSR gradient of the owned vertices [n_local, k] (partials summed by reduce-scatter)."""
         partial = self.kernels.sspmm_backward(self.row_ptr, self.col_idx, self.values,
                                               grad_local.contiguous(), idx_all,
-                                              row_div=row_div_local, plan=self.plan())
+                                              row_div=row_div_local,
+                                              plan=self.plan(idx_all.shape[1]))
         out = torch.empty(self.vmax, partial.shape[1], dtype=partial.dtype, device=partial.device)
         reduce_scatter_rows(out, partial.contiguous(), self.group)
         return out[:self.n_local]

@@ -64,7 +64,7 @@ def main(argv=None):
     ap.add_argument("--graph-dir", default=None)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--runs", type=int, default=20)
-    ap.add_argument("--bwd-mode", default="csc", choices=["csc", "atomic"])
+    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "bucket", "csc", "atomic"])
     ap.add_argument("--json", action="store_true", help="also print one JSON summary line")
     args = ap.parse_args(argv)
     if not torch.cuda.is_available():
@@ -85,7 +85,7 @@ def main(argv=None):
     V, E, D = row_ptr.numel() - 1, col.numel(), args.dim
     gen = torch.Generator(device=dev).manual_seed(123)  # main.cu:74-77
     val = torch.rand(E, generator=gen, device=dev)
-    plan = mk.transpose_plan(col, V) if args.bwd_mode == "csc" else None
+    plan = None
     print(f"# graph {args.graph} ({source}): V={V} E={E}", file=sys.stderr)
     print("num graph dim_origin dim_k kernel time(ms)")
     results = []

@@ -65,11 +65,13 @@ def test_forward_golden(mk, cuda, path, chunk):
     close(y, z["y_ref"])
 
 
-@pytest.mark.parametrize("mode", ["csc", "atomic"])
+@pytest.mark.parametrize("mode", ["auto", "bucket", "csc", "atomic"])
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_backward_golden(mk, cuda, path, chunk, mode):
     z = load_golden(path)
+    if mode == "bucket" and z["topk_idx"].shape[1] % 4:
+        pytest.skip("bucket mode needs k % 4 == 0")
     gs = mk.sspmm_backward(T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda),
                            T(z["g"], cuda), T(z["topk_idx"], cuda), row_div=T(z["deg"], cuda),
                            chunk=chunk, mode=mode)
@@ -85,6 +87,33 @@ def test_transpose_plan(mk, cuda, path):
     assert np.array_equal(col_ptr.cpu().numpy(), tp)
     order = np.argsort(z["col_idx"], kind="stable")  # CSC slot t holds CSR edge order[t]
     assert np.array_equal(eid.cpu().numpy(), order)
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_bucket_plan(mk, cuda, path):
+    """Per bucket of 2^shift columns: the CSR edge ids whose column lies in it, in CSR order,
+    and the column inside the bucket (checked against numpy)."""
+    z = load_golden(path)
+    V = z["row_ptr"].size - 1
+    col = z["col_idx"].astype(np.int64)
+    for k in (4, 16, 64):
+        bptr, beid, bdst, shift = mk.bucket_plan(T(z["col_idx"], cuda), V, k)
+        assert ((k + 1) << shift) <= 18432 < ((k + 1) << (shift + 1))
+        order = np.argsort(col >> shift, kind="stable")
+        nb = (V + (1 << shift) - 1) >> shift
+        assert np.array_equal(beid.cpu().numpy(), order)
+        assert np.array_equal(bptr.cpu().numpy(),
+                              np.searchsorted(col[order] >> shift, np.arange(nb + 1)))
+        assert np.array_equal(bdst.cpu().numpy().astype(np.int64), col[order] & ((1 << shift) - 1))
+
+
+def test_bucket_backward_repeats(mk, cuda):
+    """fp64 accumulation: two runs agree to fp32 rounding (bitwise in practice)."""
+    z = load_golden(CASES[2])
+    args = [T(z[n], cuda) for n in ("row_ptr", "col_idx", "val", "g", "topk_idx")]
+    a = mk.sspmm_backward(*args, row_div=T(z["deg"], cuda), mode="bucket")
+    b = mk.sspmm_backward(*args, row_div=T(z["deg"], cuda), mode="bucket")
+    assert torch.allclose(a, b, rtol=1e-6, atol=0)
 
 
 def test_csc_backward_is_deterministic(mk, cuda):
@@ -193,7 +222,10 @@ def test_all_k_against_oracle(mk, cuda, k, D):
     cv, ci = O.topk(x, k)
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-    for chunk, mode in ((0, "csc"), (13, "csc"), (13, "atomic")):
+    modes = [(0, "auto"), (0, "csc"), (13, "csc"), (13, "atomic")]
+    if k % 4 == 0:
+        modes.append((13, "bucket"))
+    for chunk, mode in modes:
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, chunk, mode)
         close(y, yo)
         close(gs, go)
@@ -214,9 +246,10 @@ def test_high_degree_against_oracle(mk, cuda, k):
     cv, ci = O.topk(x, k)
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-    y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, 0, "csc")
-    close(y, yo)
-    close(gs, go)
+    for mode in ("csc", "bucket") if k % 4 == 0 else ("csc",):
+        y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, 0, mode)
+        close(y, yo)
+        close(gs, go)
 
 
 def test_empty_graph_and_empty_rows(mk, cuda):
@@ -236,7 +269,7 @@ def test_empty_graph_and_empty_rows(mk, cuda):
     col = np.array([0, 5, 49], np.int32)
     val = np.array([1.0, 2.0, 3.0], np.float32)
     for chunk in (0, 1, 2, 7):
-        for mode in ("csc", "atomic"):
+        for mode in ("bucket", "csc", "atomic"):
             y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=chunk,
                                      mode=mode)
             close(y, yo)
@@ -258,7 +291,7 @@ def test_zero_rows(mk, cuda):
     y = mk.spgemm_forward(row_ptr, col, val, cv, ci, D)
     assert y.shape == (0, D)
     g = torch.zeros(0, D, device=cuda)
-    for mode in ("csc", "atomic"):
+    for mode in ("bucket", "csc", "atomic"):
         gs = torch.full((ncols, k), 7.0, device=cuda)
         mk.sspmm_backward(row_ptr, col, val, g, ci, out=gs, mode=mode)
         torch.cuda.synchronize()
@@ -277,7 +310,7 @@ def test_output_fully_overwritten(mk, cuda):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
                           D, out=out, chunk=9)
     close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, D))
-    for mode in ("csc", "atomic"):
+    for mode in ("bucket", "csc", "atomic"):
         gout = torch.full((V, k), float("nan"), device=cuda)
         gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
                                T(ci, cuda), out=gout, mode=mode, chunk=7)
@@ -307,7 +340,7 @@ def test_rectangular_shard(mk, cuda):
     val = rng.random(col.size, dtype=np.float32)
     cv, ci = O.topk(rng.standard_normal((C, D), dtype=np.float32), k)
     g = rng.standard_normal((R, D), dtype=np.float32)
-    for mode in ("csc", "atomic"):
+    for mode in ("bucket", "csc", "atomic"):
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=64, mode=mode)
         assert y.shape == (R, D) and gs.shape == (C, k)
         close(y, yo)
@@ -410,9 +443,10 @@ def test_hipgraph_capture(mk, cuda):
     close(out, z["y_ref"])
 
 
-def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch):
+@pytest.mark.parametrize("mode", ["bucket", "csc"])
+def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch, mode):
     """Default (validate-once) mode: the first call may be inside a capture; forward and the
-    deterministic backward (with its plan built beforehand) both replay correctly."""
+    two-phase backward (with its plan built beforehand) both replay correctly."""
     monkeypatch.setenv("MAXK_VALIDATE", "")
     z = load_golden(CASES[2])
     rp, ci, va, cv, cs = [T(z[n], cuda).clone() for n in ("row_ptr", "col_idx", "val", "topk_val",
@@ -422,12 +456,12 @@ def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch):
     V = rp.numel() - 1
     out = torch.empty(V, D, device=cuda)
     gs = torch.empty(cs.shape, device=cuda)
-    plan = mk.transpose_plan(ci, cs.shape[0])
+    plan = mk.backward_plan(ci, cs.shape[0], cs.shape[1], mode)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         mk.spgemm_forward(rp, ci, va, cv, cs, D, row_div=deg, out=out)
-        mk.sspmm_backward(rp, ci, va, g_in, cs, row_div=deg, out=gs, plan=plan, mode="csc")
+        mk.sspmm_backward(rp, ci, va, g_in, cs, row_div=deg, out=gs, plan=plan, mode=mode)
     out.fill_(float("nan"))
     gs.fill_(float("nan"))
     g.replay()
