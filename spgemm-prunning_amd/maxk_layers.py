@@ -92,6 +92,81 @@ def maxk(x: torch.Tensor, k: int):
     return MaxK.apply(x, k)
 
 
+# ---- dense parts of a full-graph layer (N = all vertices) ---------------------------------
+# rocBLAS / hipBLASLt pick a weight-gradient kernel for G^T X with K = N = 2.45M rows that
+# runs at ~60 TFLOP/s (5.1 ms for 256x256 on ogbn-products); as a batched GEMM over 256
+# row chunks plus a sum it takes 2.2 ms.  PyTorch's bias gradient g.sum(0) over [2.45M, 47]
+# takes 19 ms; as a chunked sum 0.11 ms (tools/dense_probe.py).  Same sums, regrouped.
+
+_CHUNKS = 256
+
+
+def _wgrad(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """g^T @ x ([O, I]) for tall g [N, O], x [N, I]."""
+    n = g.shape[0]
+    if n < _CHUNKS * 1024:
+        return g.t() @ x
+    m = n // _CHUNKS * _CHUNKS
+    out = torch.bmm(g[:m].view(_CHUNKS, m // _CHUNKS, g.shape[1]).transpose(1, 2),
+                    x[:m].view(_CHUNKS, m // _CHUNKS, x.shape[1])).sum(0)
+    if m < n:
+        out.addmm_(g[m:].t(), x[m:])
+    return out
+
+
+def _bgrad(g: torch.Tensor) -> torch.Tensor:
+    """g.sum(0) for tall g [N, O]."""
+    n = g.shape[0]
+    if n < _CHUNKS * 1024:
+        return g.sum(0)
+    m = n // _CHUNKS * _CHUNKS
+    out = g[:m].view(_CHUNKS, m // _CHUNKS, g.shape[1]).sum(1).sum(0)
+    return out + g[m:].sum(0) if m < n else out
+
+
+class _Linear(Function):
+    """out = x1 W1^T (+ x2 W2^T) (+ b): nn.Linear (or two summed, SAGE's fc_self + fc_neigh,
+    accumulated by a second addmm in place) with the tall-matrix weight/bias gradients above."""
+
+    @staticmethod
+    def forward(ctx, x1, w1, b, x2, w2):
+        out = torch.addmm(b, x1, w1.t()) if b is not None else x1 @ w1.t()
+        if x2 is not None:
+            out.addmm_(x2, w2.t())
+        ctx.save_for_backward(x1, w1, x2, w2)
+        ctx.has_b = b is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x1, w1, x2, w2 = ctx.saved_tensors
+        g = g.contiguous()
+        n = ctx.needs_input_grad
+        gx1 = g @ w1 if n[0] else None
+        gw1 = _wgrad(g, x1) if n[1] else None
+        gb = _bgrad(g) if ctx.has_b and n[2] else None
+        gx2 = g @ w2 if x2 is not None and n[3] else None
+        gw2 = _wgrad(g, x2) if x2 is not None and n[4] else None
+        return gx1, gw1, gb, gx2, gw2
+
+
+def linear(x: torch.Tensor, layer: nn.Linear, x2: Optional[torch.Tensor] = None,
+           layer2: Optional[nn.Linear] = None) -> torch.Tensor:
+    """layer(x) (+ layer2(x2)) through _Linear; layer2's bias (if any) is added separately."""
+    out = _Linear.apply(x, layer.weight, layer.bias, x2,
+                        None if layer2 is None else layer2.weight)
+    if layer2 is not None and layer2.bias is not None:
+        out = out + layer2.bias
+    return out
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """F.cross_entropy(logits, target) (mean over rows) as log_softmax + gather + mean:
+    PyTorch's nll_loss reduction kernel takes 5 ms forward + 4 ms backward on 2.45M rows,
+    this form 1.3 ms for both (tools/dense_probe.py)."""
+    return -torch.log_softmax(logits, 1).gather(1, target[:, None]).mean()
+
+
 class MaxKSAGEConv(nn.Module):
     """GraphSAGE-mean on MaxK features (model_integrated_v3.py:62-192):
     rst = fc_self(x_sparse) + fc_neigh(mean_{u in N(v)} x_sparse[u])."""
@@ -110,9 +185,9 @@ class MaxKSAGEConv(nn.Module):
 
     def forward(self, graph: CSRGraph, x_sparse, topk_values, topk_indices):
         deg = graph.in_degrees.clamp(min=1.0)
-        h_neigh = self.fc_neigh(graph.aggregate(topk_values, topk_indices, self.in_feats,
-                                                row_div=deg))
-        rst = self.fc_self(self.feat_drop(x_sparse)) + h_neigh
+        agg = graph.aggregate(topk_values, topk_indices, self.in_feats, row_div=deg)
+        # fc_self(x) + fc_neigh(agg) as one accumulated pair of GEMMs
+        rst = linear(self.feat_drop(x_sparse), self.fc_self, agg, self.fc_neigh)
         if self.activation is not None:
             rst = self.activation(rst)
         if self.norm is not None:
@@ -203,8 +278,8 @@ class MaxKSAGE(nn.Module):
         self.lin_out = nn.Linear(hid_size, out_size)
 
     def forward(self, graph: CSRGraph, x):
-        x = self.lin_in(x)
+        x = linear(x, self.lin_in)
         for layer in self.layers:
             x_sparse, vals, idx = maxk(x, self.k)
             x = layer(graph, x_sparse, vals, idx)
-        return self.lin_out(x)
+        return linear(x, self.lin_out)

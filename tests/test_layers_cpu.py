@@ -44,3 +44,38 @@ def test_aggregation_refuses_cpu_tensors():
         g.aggregate(vals, idx, 4)
     with pytest.raises(RuntimeError):
         maxk_layers.maxk(torch.rand(3, 4), 2)
+
+
+@pytest.mark.parametrize("n", [1000, 256 * 1024 + 37])
+def test_linear_tall_gradients_match_nn_linear(n):
+    """_Linear (single and the SAGE fc_self + fc_neigh pair) against nn.Linear autograd,
+    including the chunked weight / bias gradients used for N >= 256 * 1024 rows."""
+    import maxk_layers as L
+    torch.manual_seed(0)
+    a, b = torch.nn.Linear(6, 5), torch.nn.Linear(6, 5, bias=False)
+    x1 = torch.randn(n, 6, dtype=torch.float64, requires_grad=True)
+    x2 = torch.randn(n, 6, dtype=torch.float64, requires_grad=True)
+    a, b = a.double(), b.double()
+    g = torch.randn(n, 5, dtype=torch.float64)
+    ref = a(x1) + b(x2)
+    ref_grads = torch.autograd.grad(ref, [x1, x2, a.weight, a.bias, b.weight], g)
+    out = L.linear(x1, a, x2, b)
+    grads = torch.autograd.grad(out, [x1, x2, a.weight, a.bias, b.weight], g)
+    assert torch.allclose(out, ref, rtol=1e-12, atol=1e-10)
+    for got, want in zip(grads, ref_grads):
+        assert torch.allclose(got, want, rtol=1e-10, atol=1e-8)
+    single = L.linear(x1, a)
+    assert torch.allclose(single, a(x1), rtol=1e-12, atol=1e-10)
+
+
+def test_cross_entropy_matches_torch():
+    import maxk_layers as L
+    torch.manual_seed(1)
+    logits = torch.randn(500, 47, dtype=torch.float64, requires_grad=True)
+    y = torch.randint(0, 47, (500,))
+    a = L.cross_entropy(logits, y)
+    b = torch.nn.functional.cross_entropy(logits, y)
+    assert torch.allclose(a, b, rtol=1e-12)
+    ga, = torch.autograd.grad(a, logits)
+    gb, = torch.autograd.grad(b, logits)
+    assert torch.allclose(ga, gb, rtol=1e-10, atol=1e-14)
