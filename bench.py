@@ -362,6 +362,10 @@ def main():
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
         "bwd_mode": args.bwd_mode, "backward_plan_s": round(t_plan, 4),
     }
+    f_traffic, _ = load_traffic(tkey, "spgemm_forward")
+    if f_traffic:  # forward: measured (PMC) bytes per launch over its live duration
+        extra["fwd_traffic_GB"] = round(f_traffic / 1e9, 3)
+        extra["fwd_traffic_GBs"] = round(f_traffic / (fwd_avg * 1e-3) / 1e9, 1)
     if world > 1:
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
                       "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
@@ -422,7 +426,12 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "op": op, "kernels": OP_KERNELS[op],
                          "alg_bytes_per_launch": B_dom, "launch_ms": round(t_dom, 4),
-                         "traffic_source": traffic_src, "traffic_key": tkey},
+                         "traffic_source": traffic_src, "traffic_key": tkey,
+                         # measured (PMC) bytes per launch over the same live duration
+                         "traffic_GBs": (round(traffic / (t_dom * 1e-3) / 1e9, 1)
+                                         if traffic else None),
+                         "traffic_frac": (round(traffic / (t_dom * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                          if traffic else None)},
             "cpu_baseline": cpu,
             "extra": extra,
         }
