@@ -65,6 +65,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_BUCKET_PARTS  // bucketed phase 2: parts (workgroups) per CU
 #define MAXK_BUCKET_PARTS 4
 #endif
+#ifndef MAXK_TOPK_ROWS4  // top-k: 4 rows per wave on 16-lane DPP rows (0: one row per wave)
+#define MAXK_TOPK_ROWS4 1  // (used for k <= 32)
+#endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
 #endif

@@ -5,8 +5,10 @@
 // kernel topk (kernels/maxk_kernel.cu:23-96), which is approximate (quantised
 // input, index-order output, unfilled slots on ties) -- this one is exact.
 //
-// One wavefront per row (D <= 256, so <= 4 elements per lane, column
-// j = lane + 64*i for coalesced loads):
+// Two kernels.  topk_rows4_kernel (k <= 32) puts four rows on one wave, 16 lanes per row,
+// and finds the threshold by a bitwise search over DPP row sums (see its comment).
+// topk_cbsr_kernel (k > 32): one wavefront per row (D <= 256, so <= 4 elements per lane,
+// column j = lane + 64*i for coalesced loads):
 //  1. order-preserving 32-bit keys (NaN above +inf, as torch ranks it);
 //  2. the k-th largest key T by MSB-first radix select over data-adaptive
 //     8-bit digits (wave min/max of the keys in play, then a per-wave 256-bin
@@ -199,6 +201,244 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
     }
 }
 
+// ---- four rows per wave: 16 lanes per row ------------------------------------------------
+// A row lives on 16 lanes (one DPP row, 16 values per lane: columns 64i + 4q + j), so every
+// cross-lane step of a row is a DPP row operation folded into a VALU instruction and one
+// wave instruction works on four rows.  Per row: the k-th largest key by a bitwise search
+// (no LDS, no histogram atomics), tie-exact selection in column order, winners compacted to
+// LDS and ranked (key desc, column asc) against each other.  Loads are unconditional and the
+// next row group is prefetched while this one is ranked.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, true);
+}
+// all-reduce over the 16 lanes of a row (row_ror 8, 4, 2, 1)
+__device__ __forceinline__ uint32_t row_max(uint32_t x) {
+    x = max(x, dpp<0x128>(x));
+    x = max(x, dpp<0x124>(x));
+    x = max(x, dpp<0x122>(x));
+    return max(x, dpp<0x121>(x));
+}
+__device__ __forceinline__ uint32_t row_min(uint32_t x) {
+    x = min(x, dpp<0x128>(x));
+    x = min(x, dpp<0x124>(x));
+    x = min(x, dpp<0x122>(x));
+    return min(x, dpp<0x121>(x));
+}
+__device__ __forceinline__ uint32_t row_sum(uint32_t x) {
+    x += dpp<0x128>(x);
+    x += dpp<0x124>(x);
+    x += dpp<0x122>(x);
+    return x + dpp<0x121>(x);
+}
+// exclusive prefix (lanes below in the row; row_shr: lane i reads lane i-n, 0 past the row)
+__device__ __forceinline__ uint32_t row_prefix_excl(uint32_t x) {
+    uint32_t a = x;
+    a += dpp<0x111>(a);
+    a += dpp<0x112>(a);
+    a += dpp<0x114>(a);
+    a += dpp<0x118>(a);
+    return a - x;
+}
+// Unconditional loads at clamped columns (masked by ok[] afterwards): a predicated load makes
+// the compiler wait for it at the branch merge, which would expose every prefetch.
+template <typename T, bool VEC>
+__device__ __forceinline__ void load_row16(const T *__restrict__ xr, int D, int q, T (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c0 = 64 * i + 4 * q;
+        if constexpr (VEC && sizeof(T) == 4) {
+            const float4 f = *reinterpret_cast<const float4 *>(xr + (c0 < D ? c0 : D - 4));
+            v[4 * i + 0] = f.x;
+            v[4 * i + 1] = f.y;
+            v[4 * i + 2] = f.z;
+            v[4 * i + 3] = f.w;
+        } else if constexpr (VEC) {
+            const uint32_t w = *reinterpret_cast<const uint32_t *>(xr + (c0 < D ? c0 : D - 4));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * i + j] = (T)((w >> (8 * j)) & 255u);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[4 * i + j] = xr[c0 + j < D ? c0 + j : D - 1];
+        }
+    }
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict__ x, int64_t ld_x,
+                                                            T *__restrict__ out_val,
+                                                            uint8_t *__restrict__ out_idx,
+                                                            int32_t *__restrict__ out_idx32,
+                                                            T *__restrict__ out_dense,
+                                                            int num_rows, int D, int k,
+                                                            int wave_lds_words) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_topk[];
+    const int wid = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int sub = lane >> 4, q = lane & 15;
+    const int k4 = (k + 3) & ~3;
+    uint32_t *wl = lds_topk + (size_t)wid * wave_lds_words;
+    uint32_t *wkey = wl + sub * (3 * k4);  // the row's winners: keys, values, columns
+    uint32_t *wval = wkey + k4;
+    uint32_t *wcol = wval + k4;
+    const int stride = gridDim.x * kWavesPerBlock * 4;  // rows per grid step
+    bool ok[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) ok[t] = 64 * (t >> 2) + 4 * q + (t & 3) < D;
+    int row = (blockIdx.x * kWavesPerBlock + wid) * 4 + sub;
+    T vn[16];
+    load_row16<T, VEC>(x + (int64_t)(row < num_rows ? row : num_rows - 1) * ld_x, D, q, vn);
+    for (int rbase = (blockIdx.x * kWavesPerBlock + wid) * 4; rbase < num_rows;
+         rbase += stride, row += stride) {
+        const bool live = row < num_rows;
+        T v[16];
+        uint32_t key[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            v[t] = vn[t];
+            key[t] = ok[t] ? order_key(v[t]) : 0u;
+        }
+        {
+            const int nrow = row + stride;
+            load_row16<T, VEC>(x + (int64_t)(nrow < num_rows ? nrow : num_rows - 1) * ld_x, D, q,
+                               vn);
+        }
+        // ---- threshold T = the k-th largest key, built bit by bit from the highest bit where
+        // the row's keys differ: T | bit is kept while at least k keys are >= it (one compare
+        // per key and a DPP row sum per bit, no LDS).  A candidate with exactly k keys >= it
+        // ends the row's search: selecting key >= T then takes exactly k.
+        uint32_t mx = 0u, mn = ~0u;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            mx = key[t] > mx ? key[t] : mx;  // columns past D hold key 0
+            mn = ok[t] && key[t] < mn ? key[t] : mn;
+        }
+        mx = row_max(mx);
+        mn = row_min(mn);
+        const uint32_t diff = mx ^ mn;
+        int bit = diff ? 31 - __builtin_clz(diff) : -1;
+        // common prefix of the keys (all keys are >= it); bit 31 differing -> no prefix
+        uint32_t thr = !diff ? mx : (bit == 31 ? 0u : mx & (~0u << (bit + 1)));
+        bool done = !live || diff == 0u;
+        int need = k;
+        for (;;) {
+            const bool go = !done && bit >= 0;
+            if (__ballot(go) == 0) break;
+            const uint32_t c = thr | (1u << (bit & 31));
+            uint32_t n = 0;  // columns past D hold key 0 < c (c >= 1): no mask needed
+#pragma unroll
+            for (int t = 0; t < 16; ++t) n += key[t] >= c ? 1u : 0u;
+            n = row_sum(n);
+            if (go) {
+                if (n >= (uint32_t)k) thr = c;
+                if (n == (uint32_t)k) done = true;
+                --bit;
+            }
+        }
+        const int sh = 0;
+        // keys > thr are taken; `need` of the keys == thr (ties: lowest columns first)
+        {
+            uint32_t ngt = 0;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) ngt += (ok[t] && key[t] > thr) ? 1u : 0u;
+            need = k - (int)row_sum(ngt);
+        }
+        const uint32_t T_ = thr >> sh;
+        // ---- selection: key > T, plus the lowest-column keys == T until k are taken
+        uint32_t neq = 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) neq += (ok[t] && (key[t] >> sh) == T_) ? 1u : 0u;
+        const uint32_t neq_row = row_sum(neq);  // every lane: DPP reads the whole row
+        const bool ties = live && neq_row != (uint32_t)need;
+        bool take[16];
+        if (__ballot(ties) == 0) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) take[t] = ok[t] && (key[t] >> sh) >= T_;
+        } else {  // rank the equal keys in column order: chunk i, then lane, then j
+            uint32_t base = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t c = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) c += (ok[4 * i + j] && (key[4 * i + j] >> sh) == T_);
+                uint32_t r = base + row_prefix_excl(c);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int t = 4 * i + j;
+                    const bool eq = ok[t] && (key[t] >> sh) == T_;
+                    take[t] = (ok[t] && (key[t] >> sh) > T_) || (eq && r < (uint32_t)need);
+                    r += eq ? 1u : 0u;
+                }
+                base += row_sum(c);
+            }
+        }
+        if (out_dense && live) {  // fused masked dense output
+            T *dr = out_dense + (int64_t)row * D;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c0 = 64 * i + 4 * q;
+                if constexpr (sizeof(T) == 4 && VEC) {
+                    if (c0 < D) {
+                        *reinterpret_cast<float4 *>(dr + c0) =
+                            make_float4(take[4 * i] ? v[4 * i] : 0.f,
+                                        take[4 * i + 1] ? v[4 * i + 1] : 0.f,
+                                        take[4 * i + 2] ? v[4 * i + 2] : 0.f,
+                                        take[4 * i + 3] ? v[4 * i + 3] : 0.f);
+                        continue;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (c0 + j < D) dr[c0 + j] = take[4 * i + j] ? v[4 * i + j] : T(0);
+            }
+        }
+        // ---- compact the row's winners into LDS, rank them, store
+        uint32_t nw = 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) nw += take[t] ? 1u : 0u;
+        uint32_t slot = row_prefix_excl(nw);
+        wave_lds_fence();  // the previous group's winners are no longer read
+        for (int p = k + q; p < k4; p += 16) {
+            wkey[p] = 0u;
+            wcol[p] = 255u;
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            if (take[t]) {
+                wkey[slot] = key[t];
+                wval[slot] = sizeof(T) == 4 ? __builtin_bit_cast(uint32_t, (float)v[t])
+                                            : (uint32_t)v[t];
+                wcol[slot] = (uint32_t)(64 * (t >> 2) + 4 * q + (t & 3));
+                ++slot;
+            }
+        }
+        wave_lds_fence();
+        if (live) {
+            for (int p = q; p < k; p += 16) {
+                const uint32_t kp = wkey[p], cp = wcol[p];
+                int pos = 0;
+                for (int o = 0; o < k4; o += 4) {
+                    const uint4 kq = *reinterpret_cast<const uint4 *>(&wkey[o]);
+                    const uint4 cq = *reinterpret_cast<const uint4 *>(&wcol[o]);
+                    pos += (kq.x > kp) || (kq.x == kp && cq.x < cp);
+                    pos += (kq.y > kp) || (kq.y == kp && cq.y < cp);
+                    pos += (kq.z > kp) || (kq.z == kp && cq.z < cp);
+                    pos += (kq.w > kp) || (kq.w == kp && cq.w < cp);
+                }
+                const int64_t o = (int64_t)row * k + pos;
+                const uint32_t vb = wval[p];
+                if constexpr (sizeof(T) == 4)
+                    out_val[o] = __builtin_bit_cast(float, vb);
+                else
+                    out_val[o] = (T)vb;
+                out_idx[o] = (uint8_t)cp;
+                if (out_idx32) out_idx32[o] = (int32_t)cp;
+            }
+        }
+        wave_lds_fence();  // winners read before the next group's histogram overwrites them
+    }
+}
+
 // dense[r, :] = 0; dense[r, idx[r, l]] = val[r, l] + add[r, idx[r, l]]   (val and add
 // optional).  One wave per row, grid-stride: one workgroup per 4 rows would be bound by
 // workgroup dispatch on large graphs.  A row's reads all land in LDS before its stores, so
@@ -242,6 +482,25 @@ int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, 
     MAXK_REQUIRE(ld_x >= D, "ld_x (%lld) < dim_origin (%d)", (long long)ld_x, D);
     if (num_rows == 0) return MAXK_OK;
     MAXK_REQUIRE(x && val && idx, "x/val/idx must not be NULL");
+    if (MAXK_TOPK_ROWS4 && k <= 32) {  // past k=32 its k^2 ranking loses to one row per wave
+        const int k4 = (k + 3) & ~3;
+        const int words = 4 * 3 * k4;  // per wave: 4 rows of winners (key, value, column)
+        const size_t lds = (size_t)kWavesPerBlock * words * 4;
+        const bool vec = D % 4 == 0 && ld_x % 4 == 0 &&
+                         (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(T))) == 0;
+        const int64_t blocks = ceil_div(num_rows, 4 * kWavesPerBlock);
+        const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
+        if (vec)
+            hipLaunchKernelGGL((topk_rows4_kernel<T, true>), grid, dim3(kBlock), lds,
+                               as_stream(stream), x, ld_x, val, idx, idx32, dense, (int)num_rows, D,
+                               k, words);
+        else
+            hipLaunchKernelGGL((topk_rows4_kernel<T, false>), grid, dim3(kBlock), lds,
+                               as_stream(stream), x, ld_x, val, idx, idx32, dense, (int)num_rows, D,
+                               k, words);
+        MAXK_LAUNCHED("topk_rows4_kernel");
+        return MAXK_OK;
+    }
     const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
     const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
     hipLaunchKernelGGL(topk_cbsr_kernel<T>, grid, dim3(kBlock), 0, as_stream(stream), x, ld_x, val,
