@@ -399,6 +399,9 @@ def main():
             extra.update({"rocsparse_spmm_ms": round(rs, 4),
                           "speedup_fwd_vs_rocsparse": round(rs / fwd_avg, 3),
                           "speedup_bwd_vs_rocsparse": round(rs / bwd_avg, 3),
+                          # the step against two library SpMMs (A X and A^T G; the symmetric
+                          # synthetic graph gives A^T the same sparsity)
+                          "speedup_step_vs_rocsparse": round(2 * rs / (fwd_avg + bwd_avg), 3),
                           "rocsparse_vs_maxk_max_rel_err": err})
             plan.close()
             del dense

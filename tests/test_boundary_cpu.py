@@ -99,3 +99,37 @@ def test_autograd_surface_no_cpu_fallback():
         F.maxk_spgemm(idx, val, x, 2, graph_indptr=ip)
     w = F.MaxKSpmmWrapper("does_not_exist")
     assert w.load_metadata() is False  # reference contract: report and return False
+
+
+def test_backward_mode_resolution():
+    """mode "auto": bucket for k % 4 == 0, k <= 16 and >= 1/2 edge per (source row, bucket),
+    else csc; "bucket" refuses k % 4 != 0; unknown modes are rejected (no silent fallback)."""
+    import maxk_cuda_kernels as mk
+    reddit = dict(num_e=114_615_891, num_cols=232_965, num_rows=232_965)
+    products = dict(num_e=123_718_280, num_cols=2_449_029, num_rows=2_449_029)
+    assert mk._bwd_mode("auto", 16, **reddit) == "bucket"
+    assert mk._bwd_mode("auto", 8, **reddit) == "bucket"
+    assert mk._bwd_mode("auto", 32, **reddit) == "csc"
+    assert mk._bwd_mode("auto", 12, **reddit) == "bucket"
+    assert mk._bwd_mode("auto", 10, **reddit) == "csc"
+    assert mk._bwd_mode("auto", 16, **products) == "csc"
+    # a shard of 1/8 of the rows keeps Reddit's per-row degree: still bucketed
+    assert mk._bwd_mode("auto", 16, num_e=14_326_986, num_cols=232_968, num_rows=29_121) == "bucket"
+    assert mk._bwd_mode("csc", 16, **reddit) == "csc"
+    assert mk._bwd_mode("atomic", 3, **reddit) == "atomic"
+    with pytest.raises(RuntimeError):
+        mk._bwd_mode("bucket", 6, **reddit)
+    with pytest.raises(RuntimeError):
+        mk._bwd_mode("dense", 16, **reddit)
+
+
+def test_bucket_shift_rule():
+    """2^shift destinations of k + 1 doubles fill the 144 KiB fp64 LDS accumulator."""
+    from maxk_cuda_kernels import _capi
+    L = _capi.load()
+    for k in (1, 4, 8, 12, 16, 32, 64, 100, 256):
+        sh = L.maxk_bucket_shift(k)
+        assert ((k + 1) << sh) <= 18432 < ((k + 1) << (sh + 1)), k
+    assert L.maxk_bucket_shift(0) == -1
+    assert L.maxk_bucket_count(232965, 10) == 228
+    assert L.maxk_bucket_count(0, 10) == 0
