@@ -85,7 +85,6 @@ def main(argv=None):
     V, E, D = row_ptr.numel() - 1, col.numel(), args.dim
     gen = torch.Generator(device=dev).manual_seed(123)  # main.cu:74-77
     val = torch.rand(E, generator=gen, device=dev)
-    plan = None
     print(f"# graph {args.graph} ({source}): V={V} E={E}", file=sys.stderr)
     print("num graph dim_origin dim_k kernel time(ms)")
     results = []
@@ -111,12 +110,13 @@ def main(argv=None):
                                                 validate=False), args.warmup, args.runs)
         print(f"{tag} maxk {t_f:.4f}")
         t_b = time_ms(lambda: mk.sspmm_backward(row_ptr, col, val, dense, sel, out=gs,
-                                                validate=False, mode=args.bwd_mode, plan=plan),
+                                                validate=False, mode=args.bwd_mode),
                       args.warmup, args.runs)
         print(f"{tag} maxk_backward {t_b:.4f}")
         print(f"# {tag} check maxk vs library SpMM: max rel err {err:.3e} "
               f"({'PASS' if err < 1e-3 else 'FAIL'})", file=sys.stderr)
-        results.append({"k": k, "maxk_ms": t_f, "maxk_backward_ms": t_b, "max_rel_err": err,
+        results.append({"k": k, "bwd_mode": mk._bwd_mode(args.bwd_mode, k, E, V, V),
+                        "maxk_ms": t_f, "maxk_backward_ms": t_b, "max_rel_err": err,
                         "speedup_fwd": t_lib / t_f, "speedup_bwd": t_lib / t_b,
                         "gteps_fwd": E / t_f / 1e6, "gteps_bwd": E / t_b / 1e6})
         del dense, y, gs
