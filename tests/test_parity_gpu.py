@@ -107,6 +107,31 @@ def test_bucket_plan(mk, cuda, path):
         assert np.array_equal(bdst.cpu().numpy().astype(np.int64), col[order] & ((1 << shift) - 1))
 
 
+@pytest.mark.parametrize("k", [8, 16])
+def test_bucket_backward_many_parts(mk, cuda, k):
+    """A graph large enough that every bucket is cut into many parts (6M edges, parts of
+    16384 entries, ~20 parts per bucket): the slab partials and their fixup, and buckets
+    whose parts start and end mid-bucket, against the oracle."""
+    rng = np.random.default_rng(123 + k)
+    V, D, avg = 20000, 256, 300
+    deg = rng.poisson(avg, V).astype(np.int64)
+    deg[[5, 9999]] = 15000  # hubs
+    row_ptr = np.zeros(V + 1, np.int64)
+    np.cumsum(deg, out=row_ptr[1:])
+    # sorted random columns per row (vectorised: sort keys row * V + col, duplicates allowed)
+    cols = rng.integers(0, V, int(row_ptr[-1]))
+    rows = np.repeat(np.arange(V), deg)
+    col = cols[np.lexsort((cols, rows))].astype(np.int32)
+    row_ptr = row_ptr.astype(np.int32)
+    val = rng.random(col.size, dtype=np.float32)
+    _, ci = O.topk(rng.standard_normal((V, D), dtype=np.float32), k)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+    gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda),
+                           row_div=T(div, cuda), mode="bucket")
+    close(gs, O.sspmm_bwd(row_ptr, col, val, g, ci, row_div=div))
+
+
 def test_bucket_backward_repeats(mk, cuda):
     """fp64 accumulation: two runs agree to fp32 rounding (bitwise in practice)."""
     z = load_golden(CASES[2])
