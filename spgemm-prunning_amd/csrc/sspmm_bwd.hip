@@ -5,21 +5,22 @@
 // yields the A^T product) and the /out_degrees of maxk_spgemm_function.py:154-155.
 //
 // The push reads every G row once (staged in LDS) and produces one k-float
-// contribution per edge that must be summed per destination c.  Two forms of
+// contribution per edge that must be summed per destination c.  Three forms of
 // that sum:
 //  * atomic (maxk_sspmm_backward): one global fp32 atomic per (edge, l) into
 //    grad_cbsr (zeroed first).  MI355X executes float atomics memory-side and
 //    they are bound by request count: ~6 ms for Reddit-sized at any k in 2..16.
-//  * two-phase (maxk_sspmm_backward_csc, default, needs maxk_transpose_plan):
-//    phase 1 stores each edge's contribution row in CSR edge order (non-temporal
-//    16-B buffer stores, so the 7.3 GB stream does not evict the selector table
-//    every edge gathers from); phase 2 gathers the rows of each destination
-//    through the CSC permutation and sums them in a fixed order.  Bitwise
-//    deterministic; per edge one L2-resident selector lookup plus one random
-//    64-B row read, which is the floor this structure can reach.
-// Both use the token-stream work partition of common.h (one wave per item of C
-// tokens, hub rows split, short rows batched); loads-in-flight depth per launch
-// from the average degree (pick_depth).
+//  * two-phase: phase 1 stores each edge's contribution row in CSR edge order
+//    (non-temporal 16-B buffer stores, so the 7.3 GB stream does not evict the
+//    selector table every edge gathers from), then
+//    - bucket (maxk_sspmm_backward_bucket, the default for k <= 16): per bucket of
+//      destinations, the rows are read in CSR order (neighbouring rows share lines) and
+//      summed in an fp64 LDS accumulator (bucket_sum_kernel below);
+//    - csc (maxk_sspmm_backward_csc): per destination, the rows are gathered through the
+//      CSC permutation and summed in a fixed order; bitwise deterministic.
+// Phase 1 and the csc phase 2 use the token-stream work partition of common.h (one wave
+// per item of C tokens, hub rows split, short rows batched); loads-in-flight depth per
+// launch from the average degree (pick_depth).
 #include "common.h"
 
 namespace maxk {
