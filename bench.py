@@ -102,12 +102,33 @@ def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
     r1 = max(1, min(r1, len(rp) - 1))
     tf, tb = run(r1)
     es = int(rp[r1])
-    return {
+    out = {
         "value": round(2 * es / (tf + tb) / 1e9, 6), "unit": "GTEPS", "cores": 1, "kind": "port",
         "sample": (f"oracle/maxk_oracle.c fwd SpGEMM + bwd SSpMM (push), 1 thread, rows [0,{r1}) "
                    f"of the same graph = {es} of {E} edges ({100.0 * es / E:.1f}%); "
                    f"fwd {tf:.2f}s, bwd {tb:.2f}s"),
     }
+    # the same port on the host share of cores (16 on the GPU box; OpenMP), whole graph:
+    # forward over rows, backward in its pull form over the transpose (a push needs atomics)
+    import maxk_cuda_kernels as mk
+    nt = min(16, os.cpu_count() or 1)
+    col_ptr, eid = mk.transpose_plan(col, len(rp) - 1)
+    rows = torch.repeat_interleave(torch.arange(len(rp) - 1, device=col.device),
+                                   torch.diff(row_ptr).long())
+    t_ptr, t_src = col_ptr.cpu().numpy(), rows[eid.long()].int().cpu().numpy()
+    t_val = val[eid.long()].cpu().numpy()
+    del rows
+    O.set_num_threads(nt)
+    t0 = time.perf_counter()
+    O.spgemm_fwd(rp, c, v, cvn, cin, D)
+    t1 = time.perf_counter()
+    O.sspmm_bwd_pull(t_ptr, t_src, t_val, Gn, cin)
+    t2 = time.perf_counter()
+    O.set_num_threads(1)
+    out["multi_thread"] = {"value": round(2 * E / (t2 - t0) / 1e9, 6), "cores": nt,
+                           "sample": f"whole graph, {nt} OpenMP threads (backward in pull form); "
+                                     f"fwd {t1 - t0:.2f}s, bwd {t2 - t1:.2f}s"}
+    return out
 
 
 def cpu_spmm_baselines(row_ptr, col, val, dense, target_s=6.0):
