@@ -41,6 +41,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 OP_KERNELS = {
     "spgemm_forward": ["cbsr_pack_kernel", "spgemm_fwd_kernel", "slab_fixup_kernel<0>"],
     "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>"],
+    "sspmm_backward_pull": ["gprime_kernel", "pull_tile_kernel", "pull_reduce_kernel"],
     "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
 }
@@ -189,7 +190,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "bucket", "csc", "atomic"])
+    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "pull", "bucket", "csc", "atomic"])
     ap.add_argument("--graph-dir", default=None,
                     help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
     ap.add_argument("--no-cpu-spmm", action="store_true")
@@ -285,10 +286,10 @@ def main():
     # one validated call (row_ptr/col_idx/selector ranges) before the raw timed launches
     mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, validate=True)
     # per-graph setup (like the reference's warp4 files): the backward's bucket / transpose plan
-    args.bwd_mode = mk._bwd_mode(args.bwd_mode, k, El, n_cols, nl)  # "auto" -> the mode that runs
+    args.bwd_mode = mk._bwd_mode(args.bwd_mode, k, El, n_cols, nl, D)  # "auto" -> the mode that runs
     torch.cuda.synchronize()
     t_plan = time.perf_counter()
-    plan = mk.backward_plan(l_col, n_cols, k, args.bwd_mode)
+    plan = mk.backward_plan(l_col, n_cols, k, args.bwd_mode, indptr=l_row_ptr, values=l_val, dim=D)
     torch.cuda.synchronize()
     t_plan = time.perf_counter() - t_plan
 

@@ -147,6 +147,41 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
                      uint16_t *bucket_dst, void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Backward, pull form (no contribution rows): the same result as maxk_sspmm_backward,
+ * summed per tile (row slice x destination bucket of 2^shift columns) from G / row_div
+ * gathered directly, fp64 LDS accumulation, then the slices of a bucket added in slice
+ * order (deterministic).  Needs dim_k % 4 == 0, dim_origin % 4 == 0 and
+ * bucket_shift == maxk_bucket_shift(dim_k), the pull plan of the graph built with the same
+ * shift, slices and edge_val (maxk_pull_plan), and a workspace of
+ * maxk_sspmm_backward_pull_workspace_size(...) bytes (G / row_div plus slices x
+ * num_cols x k floats of tile partials).  Replaces the same reference kernels as
+ * maxk_sspmm_backward (kernels/spmm_maxk_backward.cu:15-121).
+ * ------------------------------------------------------------------------- */
+size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int64_t num_cols,
+                                               int32_t dim_origin, int32_t dim_k, int32_t slices);
+int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
+                             const uint8_t *cbsr_idx, const int32_t *tile_ptr,
+                             const int32_t *ent_row, const float *ent_w, const uint16_t *ent_dst,
+                             int32_t bucket_shift, int32_t slices, float *grad_cbsr,
+                             int64_t num_rows, int64_t num_cols, int64_t num_e,
+                             int32_t dim_origin, int32_t dim_k, void *workspace,
+                             size_t workspace_bytes, void *stream);
+
+/* Pull plan of a CSR graph and its edge values (once per graph, shift and slices):
+ * tile_ptr[slices*nb + 1] over tiles t = s*nb + j (rows cut into `slices` equal slices,
+ * nb = maxk_bucket_count(num_cols, shift)); per tile, in CSR order, ent_row / ent_w /
+ * ent_dst[num_e] = each edge's source row, edge_val and column minus the bucket's first
+ * column.  maxk_pull_slices(num_rows, dim_origin) is the default slice count (about
+ * 3.5 MiB of G rows per slice, 1..256). */
+int maxk_pull_slices(int64_t num_rows, int32_t dim_origin);
+size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                     int32_t bucket_shift, int32_t slices);
+int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                   int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t bucket_shift,
+                   int32_t slices, int32_t *tile_ptr, int32_t *ent_row, float *ent_w,
+                   uint16_t *ent_dst, void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * CBSR encode (MaxK top-k): per row the k largest of dim_origin values, in
  * torch.topk(largest=True, sorted=True) order (value descending; NaN largest;
  * equal values by ascending column).  x has leading dimension ld_x (elements).

@@ -44,6 +44,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_X4_U  // phase-1 depth; 0 = chosen per launch from the average degree
 #define MAXK_X4_U 0
 #endif
+#ifndef MAXK_PULL_U  // pull_tile_kernel: wave instructions of entries per step
+#define MAXK_PULL_U 4
+#endif
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif

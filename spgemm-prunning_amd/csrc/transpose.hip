@@ -170,3 +170,134 @@ extern "C" int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_
     MAXK_LAUNCHED("bucket_ptr_kernel");
     return MAXK_OK;
 }
+
+// ---- pull plan (the tiled pull backward, maxk_sspmm_backward_pull) -----------------------
+// Tiles t = s * n_buckets + j: rows cut into `slices` equal slices s, columns into buckets j
+// of 2^shift.  A stable radix sort of (t, edge id) lists every tile's edges in CSR order;
+// ent_row / ent_w / ent_dst are their source row, weight and column inside the bucket.
+// The weights are copied: a plan built from one `edge_val` serves that array only.
+namespace maxk {
+namespace {
+
+constexpr int64_t kPullSliceBytes = 7LL << 19;  // 3.5 MiB of G' rows per slice
+
+// one wave per row: key and source row of each of its edges
+__global__ void pull_key_kernel(const int32_t *__restrict__ row_ptr,
+                                const int32_t *__restrict__ col_idx, int num_rows,
+                                int rows_per_slice, int n_buckets, int shift,
+                                int32_t *__restrict__ keys, int32_t *__restrict__ row_of) {
+    const int r = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave);
+    if (r >= num_rows) return;
+    const int lane = lane_id();
+    const int b = row_ptr[r], e = row_ptr[r + 1];
+    const int base = (r / rows_per_slice) * n_buckets;
+    for (int i = b + lane; i < e; i += kWave) {
+        keys[i] = base + (col_idx[i] >> shift);
+        row_of[i] = r;
+    }
+}
+
+__global__ void pull_gather_kernel(const int32_t *__restrict__ eid,
+                                   const int32_t *__restrict__ row_of,
+                                   const int32_t *__restrict__ col_idx,
+                                   const float *__restrict__ edge_val, int64_t num_e, int shift,
+                                   int32_t *__restrict__ ent_row, float *__restrict__ ent_w,
+                                   uint16_t *__restrict__ ent_dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= num_e) return;
+    const int e = eid[i];
+    ent_row[i] = row_of[e];
+    ent_w[i] = edge_val[e];
+    ent_dst[i] = (uint16_t)(col_idx[e] & ((1 << shift) - 1));
+}
+
+// tile_ptr[t] = first slot with key >= t
+__global__ void tile_ptr_kernel(const int32_t *__restrict__ sorted_keys, int64_t num_e,
+                                int n_tiles, int32_t *__restrict__ tile_ptr) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > num_e) return;
+    int cur = t < num_e ? sorted_keys[t] : n_tiles;
+    int prev = t == 0 ? -1 : sorted_keys[t - 1];
+    cur = cur > n_tiles ? n_tiles : cur;  // out-of-range columns: never write past tile_ptr
+    prev = prev > n_tiles ? n_tiles : prev;
+    for (int x = prev + 1; x <= cur; ++x) tile_ptr[x] = (int32_t)t;
+}
+
+size_t pull_sort_temp_bytes(int64_t num_e, int64_t n_tiles) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t *)nullptr,
+                                             (int32_t *)nullptr, (const int32_t *)nullptr,
+                                             (int32_t *)nullptr, (int)num_e, 0,
+                                             key_bits(n_tiles));
+    return bytes;
+}
+
+}  // namespace
+}  // namespace maxk
+
+extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin) {
+    if (num_rows <= 0 || dim_origin <= 0) return 1;
+    const int64_t s = (num_rows * dim_origin * 4 + maxk::kPullSliceBytes - 1) / maxk::kPullSliceBytes;
+    return (int)(s < 1 ? 1 : (s > 256 ? 256 : s));
+}
+
+extern "C" size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                int64_t num_e, int32_t bucket_shift,
+                                                int32_t slices) {
+    if (num_rows < 0 || num_cols < 0 || num_e <= 0 || slices <= 0) return 0;
+    const int64_t nt = slices * maxk_bucket_count(num_cols, bucket_shift);
+    return 5 * al256((size_t)num_e * 4) + al256(pull_sort_temp_bytes(num_e, nt));
+}
+
+extern "C" int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx,
+                              const float *edge_val, int64_t num_rows, int64_t num_cols,
+                              int64_t num_e, int32_t bucket_shift, int32_t slices,
+                              int32_t *tile_ptr, int32_t *ent_row, float *ent_w,
+                              uint16_t *ent_dst, void *workspace, size_t workspace_bytes,
+                              void *stream) {
+    clear_error();
+    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
+    MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
+    MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
+    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 16, "bucket_shift must be in [0,16]");
+    const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
+    MAXK_REQUIRE(slices >= 1 && slices * nb < (1LL << 31), "slices %d out of range", slices);
+    MAXK_REQUIRE(tile_ptr != nullptr, "tile_ptr must not be NULL");
+    hipStream_t s = as_stream(stream);
+    const int64_t nt = slices * nb;
+    if (num_e == 0 || num_rows == 0) {
+        MAXK_HIP(hipMemsetAsync(tile_ptr, 0, (size_t)(nt + 1) * 4, s));
+        return MAXK_OK;
+    }
+    MAXK_REQUIRE(row_ptr && col_idx && edge_val && ent_row && ent_w && ent_dst,
+                 "CSR/plan pointers must not be NULL");
+    const size_t need = maxk_pull_plan_workspace_size(num_rows, num_cols, num_e, bucket_shift, slices);
+    MAXK_REQUIRE(workspace && workspace_bytes >= need, "workspace too small: need %zu", need);
+    char *ws = reinterpret_cast<char *>(workspace);
+    const size_t a = al256((size_t)num_e * 4);
+    int32_t *keys = reinterpret_cast<int32_t *>(ws);
+    int32_t *keys_out = reinterpret_cast<int32_t *>(ws + a);
+    int32_t *ids = reinterpret_cast<int32_t *>(ws + 2 * a);
+    int32_t *eid = reinterpret_cast<int32_t *>(ws + 3 * a);
+    int32_t *row_of = reinterpret_cast<int32_t *>(ws + 4 * a);
+    void *tmp = ws + 5 * a;
+    size_t tmp_bytes = workspace_bytes - 5 * a;
+    const int rps = (int)((num_rows + slices - 1) / slices);
+    hipLaunchKernelGGL(pull_key_kernel, dim3((unsigned)ceil_div(num_rows * kWave, kBlock)),
+                       dim3(kBlock), 0, s, row_ptr, col_idx, (int)num_rows, rps, (int)nb,
+                       (int)bucket_shift, keys, row_of);
+    MAXK_LAUNCHED("pull_key_kernel");
+    hipLaunchKernelGGL(iota_kernel, dim3((unsigned)ceil_div(num_e, kBlock)), dim3(kBlock), 0, s,
+                       ids, num_e);
+    MAXK_LAUNCHED("iota_kernel");
+    MAXK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_out, ids, eid,
+                                                (int)num_e, 0, key_bits(nt), s));
+    hipLaunchKernelGGL(pull_gather_kernel, dim3((unsigned)ceil_div(num_e, kBlock)), dim3(kBlock),
+                       0, s, eid, row_of, col_idx, edge_val, num_e, (int)bucket_shift, ent_row,
+                       ent_w, ent_dst);
+    MAXK_LAUNCHED("pull_gather_kernel");
+    hipLaunchKernelGGL(tile_ptr_kernel, dim3((unsigned)ceil_div(num_e + 1, kBlock)), dim3(kBlock),
+                       0, s, keys_out, num_e, (int)nt, tile_ptr);
+    MAXK_LAUNCHED("tile_ptr_kernel");
+    return MAXK_OK;
+}

@@ -40,7 +40,7 @@ __all__ = [
     "topk_cbsr", "cbsr_scatter_dense", "topk_cbsr_dense", "topk_backward",
     "build_warp4_metadata", "warp4_to_indptr",
     "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
-    "transpose_plan", "bucket_plan", "backward_plan", "BWD_MODES",
+    "transpose_plan", "bucket_plan", "pull_plan", "backward_plan", "BWD_MODES",
 ]
 
 FULL_DIM = 256  # the reference binding's fixed output width (cuda_kernel_bindings.cpp:70)
@@ -306,35 +306,96 @@ def bucket_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True
     return plan
 
 
-BWD_MODES = ("auto", "bucket", "csc", "atomic")
+_PULL_CACHE: dict = {}
+
+
+def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_cols: int,
+              k: int, dim: int = 256, slices: Optional[int] = None, cache: bool = True):
+    """(tile_ptr int32 [S*nb+1], ent_row int32 [E], ent_w f32 [E], ent_dst uint16 [E], shift,
+    S) of a CSR graph and its edge values for the pull backward at width k: rows cut into S
+    slices (default maxk_pull_slices: ~3.5 MiB of G rows each), columns into buckets of
+    2^shift; per tile (slice, bucket) the edges in CSR order with their source row, weight
+    and column inside the bucket.  Built on the GPU (one stable radix sort); cached per
+    (indices, values) tensor objects and their version counters -- the weights are copied
+    into the plan, so a plan serves the values it was built from."""
+    for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
+                     (values, "values", torch.float32)):
+        _need(t, n, dt)
+    L = _lib()
+    shift = int(L.maxk_bucket_shift(int(k)))
+    if shift < 0:
+        raise RuntimeError(f"pull_plan: invalid k {k}")
+    num_rows = indptr.numel() - 1
+    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(dim)))
+    key = (id(indices), id(values), shift, S)
+    hit = _PULL_CACHE.get(key)
+    if cache and hit is not None:
+        ri, rv, nc, vi, vv, plan = hit
+        if (ri() is indices and rv() is values and nc == num_cols and vi == indices._version
+                and vv == values._version):
+            return plan
+    dev = indices.device
+    E = indices.numel()
+    nb = int(L.maxk_bucket_count(num_cols, shift))
+    tptr = torch.empty(S * nb + 1, dtype=torch.int32, device=dev)
+    erow = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
+    ew = torch.empty(max(E, 1), dtype=torch.float32, device=dev)[:E]
+    edst = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
+    ws = torch.empty(max(1, L.maxk_pull_plan_workspace_size(num_rows, num_cols, E, shift, S)),
+                     dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(L.maxk_pull_plan(_ptr(indptr), _ptr(indices), _ptr(values), num_rows,
+                                     num_cols, E, shift, S, _ptr(tptr), _ptr(erow), _ptr(ew),
+                                     _ptr(edst), _ptr(ws), ws.numel(), _stream(dev)),
+                    "maxk_pull_plan")
+    plan = (tptr, erow, ew, edst, shift, S)
+    if cache:
+        if key not in _PULL_CACHE:
+            weakref.finalize(indices, _PULL_CACHE.pop, key, None)
+            weakref.finalize(values, _PULL_CACHE.pop, key, None)
+        _PULL_CACHE[key] = (weakref.ref(indices), weakref.ref(values), int(num_cols),
+                            indices._version, values._version, plan)
+    return plan
+
+
+BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic")
 
 
 def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0,
-              num_rows: Optional[int] = None) -> str:
-    """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) picks "bucket"
-    where it measured faster than "csc": k % 4 == 0, k <= 16 (the fp64 LDS adds grow with k
-    while contribution rows of >= 128 B gain nothing from shared lines) and at least ~1/2
-    edge per (source row, bucket) on average (Reddit k=16: 2.2; ogbn-products: 0.02)."""
+              num_rows: Optional[int] = None, dim: Optional[int] = None) -> str:
+    """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) picks "pull"
+    where it measured faster than "csc": k % 4 == 0, k <= 16 (the fp64 LDS adds grow with k)
+    and at least ~1/2 edge per (source row, bucket) on average (Reddit k=16: 2.2;
+    ogbn-products: 0.02), and dim % 4 == 0 when dim is given; "bucket" (the two-phase form
+    with the same accumulator) stays selectable."""
     mode = mode or os.environ.get("MAXK_BWD_MODE", "auto")
     if mode not in BWD_MODES:
         raise RuntimeError(f"backward mode must be one of {BWD_MODES}, got {mode!r}")
     if mode == "auto":
         mode = "csc"
-        if k % 4 == 0 and k <= 16 and num_cols > 0:
+        if k % 4 == 0 and k <= 16 and num_cols > 0 and (dim is None or dim % 4 == 0):
             shift = int(_lib().maxk_bucket_shift(int(k)))
             rows = num_rows if num_rows else num_cols
             if num_e * (1 << shift) >= rows * num_cols // 2:
-                mode = "bucket"
-    if mode == "bucket" and k % 4 != 0:
-        raise RuntimeError(f"backward mode 'bucket' needs k % 4 == 0, got k={k}")
+                mode = "pull"
+    if mode in ("bucket", "pull") and k % 4 != 0:
+        raise RuntimeError(f"backward mode {mode!r} needs k % 4 == 0, got k={k}")
+    if mode == "pull" and dim is not None and dim % 4 != 0:
+        raise RuntimeError(f"backward mode 'pull' needs dim_origin % 4 == 0, got {dim}")
     return mode
 
 
 def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[str] = None,
-                  num_rows: Optional[int] = None):
+                  num_rows: Optional[int] = None, indptr: Optional[torch.Tensor] = None,
+                  values: Optional[torch.Tensor] = None, dim: Optional[int] = None):
     """The per-graph plan sspmm_backward needs for `mode` at width k (None for "atomic");
-    num_rows (default num_cols) only steers mode "auto"."""
-    mode = _bwd_mode(mode, k, indices.numel(), num_cols, num_rows)
+    num_rows (default num_cols) and dim only steer mode "auto".  Mode "pull" also needs
+    the graph's indptr and edge values."""
+    mode = _bwd_mode(mode, k, indices.numel(), num_cols, num_rows, dim)
+    if mode == "pull":
+        if indptr is None or values is None:
+            raise RuntimeError("backward_plan: mode 'pull' needs indptr= and values=")
+        return pull_plan(indptr, indices, values, num_cols, k, dim or 256)
     if mode == "bucket":
         return bucket_plan(indices, num_cols, k)
     if mode == "csc":
@@ -349,7 +410,11 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                    mode: Optional[str] = None, plan=None) -> torch.Tensor:
     """grad_cbsr[num_cols, k] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]].
 
-    mode "auto" (default; MAXK_BWD_MODE overrides): "bucket" or "csc", see _bwd_mode.
+    mode "auto" (default; MAXK_BWD_MODE overrides): "pull" or "csc", see _bwd_mode.
+    mode "pull": per tile (row slice, destination bucket), the k values of every edge
+    gathered from G / row_div and summed in fp64 LDS accumulators, no contribution rows;
+    uses the graph's pull plan (built once per (indices, values) and cached, or `plan=`
+    from pull_plan()); deterministic.
     mode "bucket": two-phase with a bucketed phase 2 summing in fp64 LDS accumulators, using
     the graph's bucket plan (built once and cached, or `plan=` from bucket_plan()).
     mode "csc": two-phase, atomic-free and bitwise deterministic, using the graph's
@@ -378,7 +443,18 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             raise RuntimeError("out must be [num_cols, k]")
     L = _lib()
     E = indices.numel()
-    mode = _bwd_mode(mode, k, E, num_cols, num_rows)
+    mode = _bwd_mode(mode, k, E, num_cols, num_rows, D)
+    if mode == "pull":
+        tptr, erow, ew, edst, shift, S = (plan if plan is not None else
+                                          pull_plan(indptr, indices, values, num_cols, k, D))
+        ws_bytes = L.maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, D, k, S)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            _capi.check(L.maxk_sspmm_backward_pull(
+                _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tptr), _ptr(erow),
+                _ptr(ew), _ptr(edst), shift, S, _ptr(out), num_rows, num_cols, E, D, k,
+                _ptr(ws), ws.numel(), _stream(dev)), "maxk_sspmm_backward_pull")
+        return out
     if mode == "bucket":
         bptr, beid, bdst, shift = plan if plan is not None else bucket_plan(indices, num_cols, k)
         ws_bytes = L.maxk_sspmm_backward_bucket_workspace_size(num_rows, num_cols, E, D, k, chunk)

@@ -82,8 +82,9 @@ class _HipKernels:
         return self.mk.sspmm_backward(indptr, indices, values, grad, cbsr_idx, row_div=row_div,
                                       plan=plan)
 
-    def backward_plan(self, indices, num_cols, k, num_rows=None):
-        return self.mk.backward_plan(indices, num_cols, k, num_rows=num_rows)
+    def backward_plan(self, indptr, indices, values, num_cols, k, num_rows=None, dim=None):
+        return self.mk.backward_plan(indices, num_cols, k, num_rows=num_rows, indptr=indptr,
+                                     values=values, dim=dim)
 
 
 class ShardedMaxK:
@@ -133,14 +134,15 @@ class ShardedMaxK:
         idx_all = recv[:, vb:].contiguous().view(idx_local.dtype).view(self.n_cols, k)
         return val_all, idx_all
 
-    def plan(self, k: int):
-        """The backward's per-graph plan at width k (built once per k; None for a kernel
-        backend without plans, e.g. the CPU oracle in the tests)."""
-        if k not in self._plans:
+    def plan(self, k: int, D: Optional[int] = None):
+        """The backward's per-graph plan at width k and feature width D (built once per
+        (k, D); None for a kernel backend without plans, e.g. the CPU oracle in the tests)."""
+        if (k, D) not in self._plans:
             bp = getattr(self.kernels, "backward_plan", None)
-            self._plans[k] = (bp(self.col_idx, self.n_cols, k, num_rows=self.n_local)
-                              if bp is not None else None)
-        return self._plans[k]
+            self._plans[(k, D)] = (bp(self.row_ptr, self.col_idx, self.values, self.n_cols, k,
+                                      num_rows=self.n_local, dim=D)
+                                   if bp is not None else None)
+        return self._plans[(k, D)]
 
     # ---- the two aggregation passes
     def forward(self, val_all, idx_all, D: int, row_div_local=None) -> torch.Tensor:
@@ -154,7 +156,8 @@ class ShardedMaxK:
         partial = self.kernels.sspmm_backward(self.row_ptr, self.col_idx, self.values,
                                               grad_local.contiguous(), idx_all,
                                               row_div=row_div_local,
-                                              plan=self.plan(idx_all.shape[1]))
+                                              plan=self.plan(idx_all.shape[1],
+                                                             grad_local.shape[1]))
         out = torch.empty(self.vmax, partial.shape[1], dtype=partial.dtype, device=partial.device)
         reduce_scatter_rows(out, partial.contiguous(), self.group)
         return out[:self.n_local]

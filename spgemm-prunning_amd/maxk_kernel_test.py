@@ -64,7 +64,7 @@ def main(argv=None):
     ap.add_argument("--graph-dir", default=None)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--runs", type=int, default=20)
-    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "bucket", "csc", "atomic"])
+    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "pull", "bucket", "csc", "atomic"])
     ap.add_argument("--json", action="store_true", help="also print one JSON summary line")
     args = ap.parse_args(argv)
     if not torch.cuda.is_available():
@@ -115,7 +115,7 @@ def main(argv=None):
         print(f"{tag} maxk_backward {t_b:.4f}")
         print(f"# {tag} check maxk vs library SpMM: max rel err {err:.3e} "
               f"({'PASS' if err < 1e-3 else 'FAIL'})", file=sys.stderr)
-        results.append({"k": k, "bwd_mode": mk._bwd_mode(args.bwd_mode, k, E, V, V),
+        results.append({"k": k, "bwd_mode": mk._bwd_mode(args.bwd_mode, k, E, V, V, D),
                         "maxk_ms": t_f, "maxk_backward_ms": t_b, "max_rel_err": err,
                         "speedup_fwd": t_lib / t_f, "speedup_bwd": t_lib / t_b,
                         "gteps_fwd": E / t_f / 1e6, "gteps_bwd": E / t_b / 1e6})

@@ -102,23 +102,31 @@ def test_autograd_surface_no_cpu_fallback():
 
 
 def test_backward_mode_resolution():
-    """mode "auto": bucket for k % 4 == 0, k <= 16 and >= 1/2 edge per (source row, bucket),
-    else csc; "bucket" refuses k % 4 != 0; unknown modes are rejected (no silent fallback)."""
+    """mode "auto": pull for k % 4 == 0, k <= 16, dim % 4 == 0 and >= 1/2 edge per (source
+    row, bucket), else csc; "bucket" / "pull" refuse k % 4 != 0, "pull" dim % 4 != 0;
+    unknown modes are rejected (no silent fallback)."""
     import maxk_cuda_kernels as mk
     reddit = dict(num_e=114_615_891, num_cols=232_965, num_rows=232_965)
     products = dict(num_e=123_718_280, num_cols=2_449_029, num_rows=2_449_029)
-    assert mk._bwd_mode("auto", 16, **reddit) == "bucket"
-    assert mk._bwd_mode("auto", 8, **reddit) == "bucket"
+    assert mk._bwd_mode("auto", 16, **reddit) == "pull"
+    assert mk._bwd_mode("auto", 16, **reddit, dim=256) == "pull"
+    assert mk._bwd_mode("auto", 16, **reddit, dim=9) == "csc"
+    assert mk._bwd_mode("auto", 8, **reddit) == "pull"
     assert mk._bwd_mode("auto", 32, **reddit) == "csc"
-    assert mk._bwd_mode("auto", 12, **reddit) == "bucket"
+    assert mk._bwd_mode("auto", 12, **reddit) == "pull"
     assert mk._bwd_mode("auto", 10, **reddit) == "csc"
     assert mk._bwd_mode("auto", 16, **products) == "csc"
-    # a shard of 1/8 of the rows keeps Reddit's per-row degree: still bucketed
-    assert mk._bwd_mode("auto", 16, num_e=14_326_986, num_cols=232_968, num_rows=29_121) == "bucket"
+    # a shard of 1/8 of the rows keeps Reddit's per-row degree: still the pull form
+    assert mk._bwd_mode("auto", 16, num_e=14_326_986, num_cols=232_968, num_rows=29_121) == "pull"
+    assert mk._bwd_mode("bucket", 16, **reddit) == "bucket"
     assert mk._bwd_mode("csc", 16, **reddit) == "csc"
     assert mk._bwd_mode("atomic", 3, **reddit) == "atomic"
     with pytest.raises(RuntimeError):
         mk._bwd_mode("bucket", 6, **reddit)
+    with pytest.raises(RuntimeError):
+        mk._bwd_mode("pull", 6, **reddit)
+    with pytest.raises(RuntimeError):
+        mk._bwd_mode("pull", 16, **reddit, dim=9)
     with pytest.raises(RuntimeError):
         mk._bwd_mode("dense", 16, **reddit)
 
@@ -133,3 +141,18 @@ def test_bucket_shift_rule():
     assert L.maxk_bucket_shift(0) == -1
     assert L.maxk_bucket_count(232965, 10) == 228
     assert L.maxk_bucket_count(0, 10) == 0
+
+
+def test_pull_slice_rule():
+    """~3.5 MiB of G rows per slice, clamped to [1, 256]; the pull workspace is G / row_div
+    plus one fp32 partial [num_cols padded to buckets, k] per slice."""
+    from maxk_cuda_kernels import _capi
+    L = _capi.load()
+    assert L.maxk_pull_slices(232965, 256) == 66  # Reddit: 238.6 MB of G rows
+    assert L.maxk_pull_slices(29121, 256) == 9    # one of 8 row shards
+    assert L.maxk_pull_slices(1, 256) == 1 and L.maxk_pull_slices(0, 256) == 1
+    assert L.maxk_pull_slices(100_000_000, 256) == 256
+    gp = (232965 * 256 * 4 + 255) // 256 * 256
+    assert L.maxk_sspmm_backward_pull_workspace_size(232965, 232965, 256, 16, 65) == \
+        gp + 65 * 228 * (16 << 10) * 4
+    assert L.maxk_sspmm_backward_pull_workspace_size(10, 10, 0, 16, 1) == 0

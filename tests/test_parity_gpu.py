@@ -65,13 +65,15 @@ def test_forward_golden(mk, cuda, path, chunk):
     close(y, z["y_ref"])
 
 
-@pytest.mark.parametrize("mode", ["auto", "bucket", "csc", "atomic"])
+@pytest.mark.parametrize("mode", ["auto", "pull", "bucket", "csc", "atomic"])
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_backward_golden(mk, cuda, path, chunk, mode):
     z = load_golden(path)
-    if mode == "bucket" and z["topk_idx"].shape[1] % 4:
-        pytest.skip("bucket mode needs k % 4 == 0")
+    if mode in ("bucket", "pull") and z["topk_idx"].shape[1] % 4:
+        pytest.skip(f"{mode} mode needs k % 4 == 0")
+    if mode == "pull" and int(z["D"]) % 4:
+        pytest.skip("pull mode needs D % 4 == 0")
     gs = mk.sspmm_backward(T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda),
                            T(z["g"], cuda), T(z["topk_idx"], cuda), row_div=T(z["deg"], cuda),
                            chunk=chunk, mode=mode)
@@ -107,8 +109,55 @@ def test_bucket_plan(mk, cuda, path):
         assert np.array_equal(bdst.cpu().numpy().astype(np.int64), col[order] & ((1 << shift) - 1))
 
 
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_pull_plan(mk, cuda, path):
+    """Tiles t = slice(row) * nb + bucket(col): per tile the CSR edges in CSR order, with
+    their source row, weight and column inside the bucket (checked against numpy)."""
+    z = load_golden(path)
+    V = z["row_ptr"].size - 1
+    col = z["col_idx"].astype(np.int64)
+    rows = np.repeat(np.arange(V), np.diff(z["row_ptr"]))
+    for k, S in ((4, 1), (16, 3), (16, 50)):
+        tptr, erow, ew, edst, shift, s_ = mk.pull_plan(T(z["row_ptr"], cuda), T(z["col_idx"], cuda),
+                                                       T(z["val"], cuda), V, k, slices=S,
+                                                       cache=False)
+        assert s_ == S and shift == mk.bucket_plan(T(z["col_idx"], cuda), V, k)[3]
+        nb = (V + (1 << shift) - 1) >> shift
+        rps = -(-V // S)
+        key = (rows // rps) * nb + (col >> shift)
+        order = np.argsort(key, kind="stable")
+        assert np.array_equal(tptr.cpu().numpy(), np.searchsorted(key[order], np.arange(S * nb + 1)))
+        assert np.array_equal(erow.cpu().numpy(), rows[order])
+        assert np.array_equal(ew.cpu().numpy(), z["val"][order])
+        assert np.array_equal(edst.cpu().numpy().astype(np.int64), col[order] & ((1 << shift) - 1))
+
+
+def test_pull_plan_follows_values(mk, cuda):
+    """The pull plan copies the edge weights: an in-place update of `values` (version
+    counter) rebuilds it, a different values tensor gets its own plan."""
+    z = load_golden(CASES[2])
+    rp, ci, va, g, cs = [T(z[n], cuda).clone() for n in ("row_ptr", "col_idx", "val", "g",
+                                                         "topk_idx")]
+    a = mk.sspmm_backward(rp, ci, va, g, cs, mode="pull")
+    va.mul_(2.0)
+    b = mk.sspmm_backward(rp, ci, va, g, cs, mode="pull")
+    close(b, 2.0 * a.cpu().numpy())
+    c = mk.sspmm_backward(rp, ci, va * 0.5, g, cs, mode="pull")
+    close(c, a.cpu().numpy())
+
+
+def test_pull_backward_repeats(mk, cuda):
+    """fp64 tile sums, slices added in a fixed order: two runs agree to fp32 rounding."""
+    z = load_golden(CASES[2])
+    args = [T(z[n], cuda) for n in ("row_ptr", "col_idx", "val", "g", "topk_idx")]
+    a = mk.sspmm_backward(*args, row_div=T(z["deg"], cuda), mode="pull")
+    b = mk.sspmm_backward(*args, row_div=T(z["deg"], cuda), mode="pull")
+    assert torch.allclose(a, b, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("mode", ["bucket", "pull"])
 @pytest.mark.parametrize("k", [8, 16])
-def test_bucket_backward_many_parts(mk, cuda, k):
+def test_bucket_backward_many_parts(mk, cuda, k, mode):
     """A graph large enough that every bucket is cut into many parts (6M edges, parts of
     16384 entries, ~20 parts per bucket): the slab partials and their fixup, and buckets
     whose parts start and end mid-bucket, against the oracle."""
@@ -128,8 +177,17 @@ def test_bucket_backward_many_parts(mk, cuda, k):
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
     gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda),
-                           row_div=T(div, cuda), mode="bucket")
-    close(gs, O.sspmm_bwd(row_ptr, col, val, g, ci, row_div=div))
+                           row_div=T(div, cuda), mode=mode)
+    go = O.sspmm_bwd(row_ptr, col, val, g, ci, row_div=div)
+    close(gs, go)
+    if mode == "pull":  # other slicings of the same graph: 1, 7 and 100 row slices
+        tc, vc = T(col, cuda), T(val, cuda)
+        for S in (1, 7, 100):
+            plan = mk.pull_plan(T(row_ptr, cuda), tc, vc, V, k, D, slices=S, cache=False)
+            assert plan[5] == S
+            gs = mk.sspmm_backward(T(row_ptr, cuda), tc, vc, T(g, cuda), T(ci, cuda),
+                                   row_div=T(div, cuda), mode="pull", plan=plan)
+            close(gs, go)
 
 
 def test_bucket_backward_repeats(mk, cuda):
@@ -250,6 +308,8 @@ def test_all_k_against_oracle(mk, cuda, k, D):
     modes = [(0, "auto"), (0, "csc"), (13, "csc"), (13, "atomic")]
     if k % 4 == 0:
         modes.append((13, "bucket"))
+        if D % 4 == 0:
+            modes.append((0, "pull"))
     for chunk, mode in modes:
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, chunk, mode)
         close(y, yo)
@@ -271,7 +331,7 @@ def test_high_degree_against_oracle(mk, cuda, k):
     cv, ci = O.topk(x, k)
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-    for mode in ("csc", "bucket") if k % 4 == 0 else ("csc",):
+    for mode in ("csc", "bucket", "pull") if k % 4 == 0 else ("csc",):
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, 0, mode)
         close(y, yo)
         close(gs, go)
@@ -294,7 +354,7 @@ def test_empty_graph_and_empty_rows(mk, cuda):
     col = np.array([0, 5, 49], np.int32)
     val = np.array([1.0, 2.0, 3.0], np.float32)
     for chunk in (0, 1, 2, 7):
-        for mode in ("bucket", "csc", "atomic"):
+        for mode in ("pull", "bucket", "csc", "atomic"):
             y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=chunk,
                                      mode=mode)
             close(y, yo)
@@ -316,7 +376,7 @@ def test_zero_rows(mk, cuda):
     y = mk.spgemm_forward(row_ptr, col, val, cv, ci, D)
     assert y.shape == (0, D)
     g = torch.zeros(0, D, device=cuda)
-    for mode in ("bucket", "csc", "atomic"):
+    for mode in ("pull", "bucket", "csc", "atomic"):
         gs = torch.full((ncols, k), 7.0, device=cuda)
         mk.sspmm_backward(row_ptr, col, val, g, ci, out=gs, mode=mode)
         torch.cuda.synchronize()
@@ -335,7 +395,7 @@ def test_output_fully_overwritten(mk, cuda):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
                           D, out=out, chunk=9)
     close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, D))
-    for mode in ("bucket", "csc", "atomic"):
+    for mode in ("pull", "bucket", "csc", "atomic"):
         gout = torch.full((V, k), float("nan"), device=cuda)
         gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
                                T(ci, cuda), out=gout, mode=mode, chunk=7)
@@ -365,7 +425,7 @@ def test_rectangular_shard(mk, cuda):
     val = rng.random(col.size, dtype=np.float32)
     cv, ci = O.topk(rng.standard_normal((C, D), dtype=np.float32), k)
     g = rng.standard_normal((R, D), dtype=np.float32)
-    for mode in ("bucket", "csc", "atomic"):
+    for mode in ("pull", "bucket", "csc", "atomic"):
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=64, mode=mode)
         assert y.shape == (R, D) and gs.shape == (C, k)
         close(y, yo)
@@ -468,7 +528,7 @@ def test_hipgraph_capture(mk, cuda):
     close(out, z["y_ref"])
 
 
-@pytest.mark.parametrize("mode", ["bucket", "csc"])
+@pytest.mark.parametrize("mode", ["pull", "bucket", "csc"])
 def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch, mode):
     """Default (validate-once) mode: the first call may be inside a capture; forward and the
     two-phase backward (with its plan built beforehand) both replay correctly."""
@@ -481,7 +541,7 @@ def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch, mode):
     V = rp.numel() - 1
     out = torch.empty(V, D, device=cuda)
     gs = torch.empty(cs.shape, device=cuda)
-    plan = mk.backward_plan(ci, cs.shape[0], cs.shape[1], mode)
+    plan = mk.backward_plan(ci, cs.shape[0], cs.shape[1], mode, indptr=rp, values=va, dim=D)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
