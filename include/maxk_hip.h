@@ -173,6 +173,7 @@ int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
  * ent_dst[num_e] = each edge's source row, edge_val and column minus the bucket's first
  * column.  maxk_pull_slices(num_rows, dim_origin) is the default slice count (about
  * 3.5 MiB of G rows per slice, 1..256). */
+int maxk_pull_shift(int32_t dim_k);
 int maxk_pull_slices(int64_t num_rows, int32_t dim_origin);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
                                      int32_t bucket_shift, int32_t slices);

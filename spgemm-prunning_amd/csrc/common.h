@@ -44,6 +44,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_X4_U  // phase-1 depth; 0 = chosen per launch from the average degree
 #define MAXK_X4_U 0
 #endif
+#ifndef MAXK_PULL_SHIFT_DELTA  // pull buckets of 2^(maxk_bucket_shift(k) - delta) columns
+#define MAXK_PULL_SHIFT_DELTA 0
+#endif
 #ifndef MAXK_PULL_U  // pull_tile_kernel: wave instructions of entries per step
 #define MAXK_PULL_U 4
 #endif

@@ -574,7 +574,7 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
     const int32_t *__restrict__ tile_ptr, const int32_t *__restrict__ ent_row,
     const float *__restrict__ ent_w, const uint16_t *__restrict__ ent_dst,
     float *__restrict__ tile_out, int n_buckets, int D, int k, int shift) {
-    __shared__ double acc[kBucketAccDoubles];
+    extern __shared__ double acc[];  // [(k + 1) << shift]
     constexpr int EPI = kWave / LR;
     constexpr int STEP = EPI * U;
     const int tid = threadIdx.x;
@@ -997,7 +997,7 @@ extern "C" size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int6
                                                           int32_t dim_origin, int32_t dim_k,
                                                           int32_t slices) {
     if (num_rows < 0 || num_cols < 0 || dim_origin <= 0 || dim_k <= 0 || slices <= 0) return 0;
-    const int shift = maxk_bucket_shift(dim_k);
+    const int shift = maxk_bucket_shift(dim_k);  // the largest shift: bounds every plan's
     const int64_t nb = maxk_bucket_count(num_cols, shift);
     const size_t gp = ((size_t)num_rows * dim_origin * sizeof(float) + 255) & ~(size_t)255;
     return gp + (size_t)slices * nb * ((size_t)dim_k << shift) * sizeof(float);
@@ -1016,9 +1016,9 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     MAXK_REQUIRE(dim_k % 4 == 0, "pull backward needs dim_k %% 4 == 0, got %d", dim_k);
     MAXK_REQUIRE(dim_origin % 4 == 0, "pull backward needs dim_origin %% 4 == 0, got %d",
                  dim_origin);
-    MAXK_REQUIRE(bucket_shift == maxk_bucket_shift(dim_k),
-                 "bucket_shift %d does not match maxk_bucket_shift(%d) = %d", bucket_shift, dim_k,
-                 maxk_bucket_shift(dim_k));
+    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= maxk_bucket_shift(dim_k),
+                 "bucket_shift %d out of range [0, maxk_bucket_shift(%d) = %d]", bucket_shift,
+                 dim_k, maxk_bucket_shift(dim_k));
     const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
     MAXK_REQUIRE(slices >= 1 && slices * nb < (1LL << 31), "slices %d out of range", slices);
     hipStream_t s = as_stream(stream);
@@ -1043,10 +1043,11 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     }
     float *tile_out = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + gpb);
     const unsigned tiles = (unsigned)(slices * nb);
+    const size_t lds = ((size_t)(k + 1) << bucket_shift) * sizeof(double);
     switch (lanes_per_edge(k / 4)) {
 #define MAXK_CASE(LRV)                                                                        \
     case LRV:                                                                                 \
-        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U>), dim3(tiles), dim3(1024), 0, s, \
+        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U>), dim3(tiles), dim3(1024), lds, s, \
                            Gp, cbsr_idx, tile_ptr, ent_row, ent_w, ent_dst, tile_out, (int)nb, \
                            dim_origin, k, bucket_shift);                                      \
         break;

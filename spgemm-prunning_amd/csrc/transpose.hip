@@ -235,6 +235,11 @@ size_t pull_sort_temp_bytes(int64_t num_e, int64_t n_tiles) {
 }  // namespace
 }  // namespace maxk
 
+extern "C" int maxk_pull_shift(int32_t dim_k) {
+    const int s = maxk_bucket_shift(dim_k);
+    return s < 0 ? s : (s > MAXK_PULL_SHIFT_DELTA ? s - MAXK_PULL_SHIFT_DELTA : 0);
+}
+
 extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
     const int64_t s = (num_rows * dim_origin * 4 + maxk::kPullSliceBytes - 1) / maxk::kPullSliceBytes;

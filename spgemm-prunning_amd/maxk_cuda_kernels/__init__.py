@@ -322,7 +322,7 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
                      (values, "values", torch.float32)):
         _need(t, n, dt)
     L = _lib()
-    shift = int(L.maxk_bucket_shift(int(k)))
+    shift = int(L.maxk_pull_shift(int(k)))
     if shift < 0:
         raise RuntimeError(f"pull_plan: invalid k {k}")
     num_rows = indptr.numel() - 1

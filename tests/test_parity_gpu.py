@@ -121,7 +121,7 @@ def test_pull_plan(mk, cuda, path):
         tptr, erow, ew, edst, shift, s_ = mk.pull_plan(T(z["row_ptr"], cuda), T(z["col_idx"], cuda),
                                                        T(z["val"], cuda), V, k, slices=S,
                                                        cache=False)
-        assert s_ == S and shift == mk.bucket_plan(T(z["col_idx"], cuda), V, k)[3]
+        assert s_ == S and shift == mk._lib().maxk_pull_shift(k)
         nb = (V + (1 << shift) - 1) >> shift
         rps = -(-V // S)
         key = (rows // rps) * nb + (col >> shift)

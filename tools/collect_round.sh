@@ -1,7 +1,7 @@
 #!/bin/bash
 # Copy one gpu_round.sh run (gpurun_out/rNN) into profiles/rNN and regenerate the summaries.
 set -e
-R=${1:-r01}; KEY=${2:-reddit-D256-k16-bucket-n1}
+R=${1:-r01}; KEY=${2:-reddit-D256-k16-pull-n1}
 cd "$(dirname "$0")/.."
 O=gpurun_out/$R; P=profiles/$R
 mkdir -p $P/stats_bench
