@@ -110,7 +110,7 @@ int maxk_transpose_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
                         size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
- * Same backward, two-phase with a bucketed phase 2 (the default for k % 4 == 0):
+ * Same backward, two-phase with a bucketed phase 2 (k % 4 == 0):
  * phase 1 as in maxk_sspmm_backward_csc; phase 2 gives every bucket of 2^bucket_shift
  * consecutive destinations one workgroup, which reads the bucket's contribution rows in
  * CSR order (neighbouring rows share cache lines) and sums them in an fp64 LDS

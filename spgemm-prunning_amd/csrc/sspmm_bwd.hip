@@ -4,18 +4,22 @@
 // Semantics: kernels/spmm_maxk_backward.cu:15-115 (push from the CSR of A, which
 // yields the A^T product) and the /out_degrees of maxk_spgemm_function.py:154-155.
 //
-// The push reads every G row once (staged in LDS) and produces one k-float
-// contribution per edge that must be summed per destination c.  Three forms of
-// that sum:
-//  * atomic (maxk_sspmm_backward): one global fp32 atomic per (edge, l) into
-//    grad_cbsr (zeroed first).  MI355X executes float atomics memory-side and
-//    they are bound by request count: ~6 ms for Reddit-sized at any k in 2..16.
-//  * two-phase: phase 1 stores each edge's contribution row in CSR edge order
+// Every edge needs the k values of its source row's G picked by its destination's
+// selectors, summed per destination c.  Four forms of that sum:
+//  * pull (maxk_sspmm_backward_pull, the default for k % 4 == 0, k <= 16 on dense graphs):
+//    per tile (row slice, destination bucket) the edges' values are gathered straight from
+//    G / row_div into an fp64 LDS accumulator; no per-edge contribution rows
+//    (pull_tile_kernel below).
+//  * atomic (maxk_sspmm_backward): the push, each G row staged once in LDS and one global
+//    fp32 atomic per (edge, l) into grad_cbsr (zeroed first).  MI355X executes float
+//    atomics memory-side and they are bound by request count: ~6 ms for Reddit-sized at
+//    any k in 2..16.
+//  * two-phase: phase 1 (the push) stores each edge's contribution row in CSR edge order
 //    (non-temporal 16-B buffer stores, so the 7.3 GB stream does not evict the
 //    selector table every edge gathers from), then
-//    - bucket (maxk_sspmm_backward_bucket, the default for k <= 16): per bucket of
-//      destinations, the rows are read in CSR order (neighbouring rows share lines) and
-//      summed in an fp64 LDS accumulator (bucket_sum_kernel below);
+//    - bucket (maxk_sspmm_backward_bucket): per bucket of destinations, the rows are read
+//      in CSR order (neighbouring rows share lines) and summed in an fp64 LDS accumulator
+//      (bucket_sum_kernel below);
 //    - csc (maxk_sspmm_backward_csc): per destination, the rows are gathered through the
 //      CSC permutation and summed in a fixed order; bitwise deterministic.
 // Phase 1 and the csc phase 2 use the token-stream work partition of common.h (one wave
