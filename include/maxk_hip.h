@@ -161,26 +161,26 @@ size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int64_t num_col
                                                int32_t dim_origin, int32_t dim_k, int32_t slices);
 int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
                              const uint8_t *cbsr_idx, const int32_t *tile_ptr,
-                             const int32_t *ent_row, const float *ent_w, const uint16_t *ent_dst,
-                             int32_t bucket_shift, int32_t slices, float *grad_cbsr,
-                             int64_t num_rows, int64_t num_cols, int64_t num_e,
+                             const uint32_t *ent, int32_t bucket_shift, int32_t slices,
+                             float *grad_cbsr, int64_t num_rows, int64_t num_cols, int64_t num_e,
                              int32_t dim_origin, int32_t dim_k, void *workspace,
                              size_t workspace_bytes, void *stream);
 
 /* Pull plan of a CSR graph and its edge values (once per graph, shift and slices):
- * tile_ptr[slices*nb + 1] over tiles t = s*nb + j (rows cut into `slices` equal slices,
- * nb = maxk_bucket_count(num_cols, shift)); per tile, in CSR order, ent_row / ent_w /
- * ent_dst[num_e] = each edge's source row, edge_val and column minus the bucket's first
- * column.  maxk_pull_slices(num_rows, dim_origin) is the default slice count (about
- * 3.5 MiB of G rows per slice, 1..256). */
+ * tile_ptr[slices*nb + 1] over tiles t = s*nb + j (rows cut into `slices` slices of
+ * ceil(num_rows/slices) <= 65536 rows, nb = maxk_bucket_count(num_cols, shift)); per tile,
+ * in CSR order, ent[2*num_e] = one uint32 pair per edge: {row - first row of its slice |
+ * (column - first column of its bucket) << 16, bits of edge_val}.  maxk_pull_shift(k) is
+ * the bucket shift to use; maxk_pull_slices(num_rows, dim_origin) the default slice count
+ * (about 3.5 MiB of G rows per slice, at least num_rows/65536, 1..256). */
 int maxk_pull_shift(int32_t dim_k);
 int maxk_pull_slices(int64_t num_rows, int32_t dim_origin);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
                                      int32_t bucket_shift, int32_t slices);
 int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
                    int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t bucket_shift,
-                   int32_t slices, int32_t *tile_ptr, int32_t *ent_row, float *ent_w,
-                   uint16_t *ent_dst, void *workspace, size_t workspace_bytes, void *stream);
+                   int32_t slices, int32_t *tile_ptr, uint32_t *ent, void *workspace,
+                   size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * CBSR encode (MaxK top-k): per row the k largest of dim_origin values, in

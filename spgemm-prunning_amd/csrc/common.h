@@ -47,6 +47,7 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_PULL_SHIFT_DELTA  // pull buckets of 2^(maxk_bucket_shift(k) - delta) columns
 #define MAXK_PULL_SHIFT_DELTA 0
 #endif
+constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_U  // pull_tile_kernel: wave instructions of entries per step
 #define MAXK_PULL_U 4
 #endif

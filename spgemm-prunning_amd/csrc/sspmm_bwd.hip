@@ -569,16 +569,18 @@ __global__ __launch_bounds__(kBlock) void gprime_kernel(const float *__restrict_
     reinterpret_cast<float4 *>(Gp)[i] = v;
 }
 
-// LR = pow2ceil(k/4) lanes per entry, lane q owning l = 4q..4q+3 (one u32 selector load,
-// four gathers, four LDS adds); 64/LR entries per wave instruction, U instructions per
-// wave step, the next step's entries prefetched.
-template <int LR, int U>
+// LR = pow2ceil(k/4) lanes per entry, lane q owning l = 4q..4q+3: per entry one 8-B entry
+// load, one u32 selector read (from LDS when the bucket's selector rows fit next to the
+// accumulator, SEL_LDS), four gathers and four LDS adds; 64/LR entries per wave
+// instruction, U instructions per wave step, the next step's entries prefetched.
+// Entry = {row within the slice | column within the bucket << 16, weight bits}.
+template <int LR, int U, bool SEL_LDS>
 __global__ __launch_bounds__(1024) void pull_tile_kernel(
     const float *__restrict__ Gp, const uint8_t *__restrict__ cbsr_idx,
-    const int32_t *__restrict__ tile_ptr, const int32_t *__restrict__ ent_row,
-    const float *__restrict__ ent_w, const uint16_t *__restrict__ ent_dst,
-    float *__restrict__ tile_out, int n_buckets, int D, int k, int shift) {
-    extern __shared__ double acc[];  // [(k + 1) << shift]
+    const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
+    float *__restrict__ tile_out, int64_t num_cols, int n_buckets, int rows_per_slice, int D,
+    int k, int shift) {
+    extern __shared__ double acc[];  // [(k + 1) << shift], then (SEL_LDS) [k << shift] bytes
     constexpr int EPI = kWave / LR;
     constexpr int STEP = EPI * U;
     const int tid = threadIdx.x;
@@ -589,42 +591,46 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
     const int ks = k + 1;
     const int t = blockIdx.x;
     const int j = t % n_buckets;
+    const float *__restrict__ Gs = Gp + (size_t)(t / n_buckets) * rows_per_slice * D;
     const int s0 = tile_ptr[t], s1 = tile_ptr[t + 1];
+    const int64_t c0 = (int64_t)j << shift;
+    const uint32_t *__restrict__ selg = reinterpret_cast<const uint32_t *>(cbsr_idx + c0 * k);
+    uint32_t *sel_lds = reinterpret_cast<uint32_t *>(acc + (ks << shift));
     for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
+    if (SEL_LDS) {
+        const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
+        for (int i = tid; i < rows * kq; i += 1024) sel_lds[i] = selg[i];
+    }
     __syncthreads();
-    const uint32_t *__restrict__ selb =
-        reinterpret_cast<const uint32_t *>(cbsr_idx + ((size_t)j << shift) * k);
     int base = s0 + w * STEP;
-    int r[U], d[U];
-    float wt[U];
+    uint2 en[U];
     auto load_ids = [&](int b) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int e = b + u * EPI + g;
-            const int ec = e < s1 ? e : s1 - 1;
-            r[u] = ent_row[ec];
-            wt[u] = ent_w[ec];
-            d[u] = e < s1 ? (int)ent_dst[ec] : -1;
+            en[u] = ent[e < s1 ? e : s1 - 1];
+            if (e >= s1) en[u].x = 0xffff0000u;  // no entry: row 0 (a valid gather), column 0xffff
         }
     };
     if (base < s1) load_ids(base);
     for (; base < s1; base += 16 * STEP) {
         uint32_t sv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) sv[u] = selb[(d[u] < 0 ? 0 : d[u]) * kq + (qok ? q : 0)];
-        float v[U][4];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float *gr = Gp + (size_t)(uint32_t)r[u] * (uint32_t)D;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[u][i] = gr[(sv[u] >> (8 * i)) & 255u];
-        }
         int dc[U];
         float wc[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            dc[u] = d[u];
-            wc[u] = wt[u];
+            const uint32_t key = en[u].x;
+            dc[u] = (key >> 16) == 0xffffu ? -1 : (int)(key >> 16);
+            const int si = (dc[u] < 0 ? 0 : dc[u]) * kq + (qok ? q : 0);
+            sv[u] = SEL_LDS ? sel_lds[si] : selg[si];
+        }
+        float v[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float *gr = Gs + (en[u].x & 0xffffu) * (uint32_t)D;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[u][i] = gr[(sv[u] >> (8 * i)) & 255u];
+            wc[u] = __uint_as_float(en[u].y);
         }
         if (base + 16 * STEP < s1) load_ids(base + 16 * STEP);
 #pragma unroll
@@ -1009,8 +1015,7 @@ extern "C" size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int6
 
 extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
                                         const uint8_t *cbsr_idx, const int32_t *tile_ptr,
-                                        const int32_t *ent_row, const float *ent_w,
-                                        const uint16_t *ent_dst, int32_t bucket_shift,
+                                        const uint32_t *ent, int32_t bucket_shift,
                                         int32_t slices, float *grad_cbsr, int64_t num_rows,
                                         int64_t num_cols, int64_t num_e, int32_t dim_origin,
                                         int32_t dim_k, void *workspace, size_t workspace_bytes,
@@ -1020,15 +1025,19 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     MAXK_REQUIRE(dim_k % 4 == 0, "pull backward needs dim_k %% 4 == 0, got %d", dim_k);
     MAXK_REQUIRE(dim_origin % 4 == 0, "pull backward needs dim_origin %% 4 == 0, got %d",
                  dim_origin);
-    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= maxk_bucket_shift(dim_k),
-                 "bucket_shift %d out of range [0, maxk_bucket_shift(%d) = %d]", bucket_shift,
-                 dim_k, maxk_bucket_shift(dim_k));
+    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= maxk_bucket_shift(dim_k) &&
+                     bucket_shift <= 15,
+                 "bucket_shift %d out of range [0, min(15, maxk_bucket_shift(%d) = %d)]",
+                 bucket_shift, dim_k, maxk_bucket_shift(dim_k));
     const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
     MAXK_REQUIRE(slices >= 1 && slices * nb < (1LL << 31), "slices %d out of range", slices);
+    const int64_t rps = (num_rows + slices - 1) / slices;
+    MAXK_REQUIRE(rps <= 65536, "%d slices leave %lld rows per slice (max 65536)", slices,
+                 (long long)rps);
     hipStream_t s = as_stream(stream);
     if (num_cols == 0) return MAXK_OK;
     MAXK_REQUIRE(grad_cbsr && tile_ptr, "grad_cbsr/tile_ptr must not be NULL");
-    MAXK_REQUIRE(num_e == 0 || (grad_out && cbsr_idx && ent_row && ent_w && ent_dst),
+    MAXK_REQUIRE(num_e == 0 || (grad_out && cbsr_idx && ent),
                  "grad/selector/plan pointers must not be NULL");
     const size_t need =
         maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, dim_origin, dim_k, slices);
@@ -1047,21 +1056,25 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     }
     float *tile_out = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + gpb);
     const unsigned tiles = (unsigned)(slices * nb);
-    const size_t lds = ((size_t)(k + 1) << bucket_shift) * sizeof(double);
-    switch (lanes_per_edge(k / 4)) {
-#define MAXK_CASE(LRV)                                                                        \
-    case LRV:                                                                                 \
-        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U>), dim3(tiles), dim3(1024), lds, s, \
-                           Gp, cbsr_idx, tile_ptr, ent_row, ent_w, ent_dst, tile_out, (int)nb, \
-                           dim_origin, k, bucket_shift);                                      \
+    const size_t acc_b = ((size_t)(k + 1) << bucket_shift) * sizeof(double);
+    const size_t sel_b = ((size_t)k << bucket_shift);
+    const bool sel_lds = acc_b + sel_b <= kPullLdsBytes;
+    const size_t lds = acc_b + (sel_lds ? sel_b : 0);
+    const uint2 *ent2 = reinterpret_cast<const uint2 *>(ent);
+    switch (lanes_per_edge(k / 4) * 2 + (sel_lds ? 1 : 0)) {
+#define MAXK_CASE(LRV, SL)                                                                    \
+    case LRV * 2 + SL:                                                                        \
+        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL>), dim3(tiles), dim3(1024),  \
+                           lds, s, Gp, cbsr_idx, tile_ptr, ent2, tile_out, num_cols, (int)nb,  \
+                           (int)rps, dim_origin, k, bucket_shift);                            \
         break;
-        MAXK_CASE(1)
-        MAXK_CASE(2)
-        MAXK_CASE(4)
-        MAXK_CASE(8)
-        MAXK_CASE(16)
-        MAXK_CASE(32)
-        MAXK_CASE(64)
+        MAXK_CASE(1, 0) MAXK_CASE(1, 1)
+        MAXK_CASE(2, 0) MAXK_CASE(2, 1)
+        MAXK_CASE(4, 0) MAXK_CASE(4, 1)
+        MAXK_CASE(8, 0) MAXK_CASE(8, 1)
+        MAXK_CASE(16, 0) MAXK_CASE(16, 1)
+        MAXK_CASE(32, 0) MAXK_CASE(32, 1)
+        MAXK_CASE(64, 0) MAXK_CASE(64, 1)
 #undef MAXK_CASE
         default:
             set_error("unsupported lane group");

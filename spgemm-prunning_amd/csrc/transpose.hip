@@ -201,14 +201,14 @@ __global__ void pull_gather_kernel(const int32_t *__restrict__ eid,
                                    const int32_t *__restrict__ row_of,
                                    const int32_t *__restrict__ col_idx,
                                    const float *__restrict__ edge_val, int64_t num_e, int shift,
-                                   int32_t *__restrict__ ent_row, float *__restrict__ ent_w,
-                                   uint16_t *__restrict__ ent_dst) {
+                                   int rows_per_slice, uint2 *__restrict__ ent) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= num_e) return;
     const int e = eid[i];
-    ent_row[i] = row_of[e];
-    ent_w[i] = edge_val[e];
-    ent_dst[i] = (uint16_t)(col_idx[e] & ((1 << shift) - 1));
+    const int r = row_of[e];
+    const uint32_t in_slice = (uint32_t)(r % rows_per_slice);
+    const uint32_t dst = (uint32_t)(col_idx[e] & ((1 << shift) - 1));
+    ent[i] = make_uint2(in_slice | (dst << 16), __float_as_uint(edge_val[e]));
 }
 
 // tile_ptr[t] = first slot with key >= t
@@ -242,7 +242,9 @@ extern "C" int maxk_pull_shift(int32_t dim_k) {
 
 extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
-    const int64_t s = (num_rows * dim_origin * 4 + maxk::kPullSliceBytes - 1) / maxk::kPullSliceBytes;
+    int64_t s = (num_rows * dim_origin * 4 + maxk::kPullSliceBytes - 1) / maxk::kPullSliceBytes;
+    const int64_t lo = (num_rows + 65535) / 65536;  // rows within a slice fit 16 bits
+    s = s < lo ? lo : s;
     return (int)(s < 1 ? 1 : (s > 256 ? 256 : s));
 }
 
@@ -257,16 +259,18 @@ extern "C" size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_co
 extern "C" int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx,
                               const float *edge_val, int64_t num_rows, int64_t num_cols,
                               int64_t num_e, int32_t bucket_shift, int32_t slices,
-                              int32_t *tile_ptr, int32_t *ent_row, float *ent_w,
-                              uint16_t *ent_dst, void *workspace, size_t workspace_bytes,
-                              void *stream) {
+                              int32_t *tile_ptr, uint32_t *ent, void *workspace,
+                              size_t workspace_bytes, void *stream) {
     clear_error();
     MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
     MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
     MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
-    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 16, "bucket_shift must be in [0,16]");
+    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 15, "bucket_shift must be in [0,15]");
     const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
     MAXK_REQUIRE(slices >= 1 && slices * nb < (1LL << 31), "slices %d out of range", slices);
+    const int64_t rps64 = (num_rows + slices - 1) / slices;
+    MAXK_REQUIRE(rps64 <= 65536, "%d slices leave %lld rows per slice (max 65536)", slices,
+                 (long long)rps64);
     MAXK_REQUIRE(tile_ptr != nullptr, "tile_ptr must not be NULL");
     hipStream_t s = as_stream(stream);
     const int64_t nt = slices * nb;
@@ -274,8 +278,7 @@ extern "C" int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx,
         MAXK_HIP(hipMemsetAsync(tile_ptr, 0, (size_t)(nt + 1) * 4, s));
         return MAXK_OK;
     }
-    MAXK_REQUIRE(row_ptr && col_idx && edge_val && ent_row && ent_w && ent_dst,
-                 "CSR/plan pointers must not be NULL");
+    MAXK_REQUIRE(row_ptr && col_idx && edge_val && ent, "CSR/plan pointers must not be NULL");
     const size_t need = maxk_pull_plan_workspace_size(num_rows, num_cols, num_e, bucket_shift, slices);
     MAXK_REQUIRE(workspace && workspace_bytes >= need, "workspace too small: need %zu", need);
     char *ws = reinterpret_cast<char *>(workspace);
@@ -287,7 +290,7 @@ extern "C" int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx,
     int32_t *row_of = reinterpret_cast<int32_t *>(ws + 4 * a);
     void *tmp = ws + 5 * a;
     size_t tmp_bytes = workspace_bytes - 5 * a;
-    const int rps = (int)((num_rows + slices - 1) / slices);
+    const int rps = (int)rps64;
     hipLaunchKernelGGL(pull_key_kernel, dim3((unsigned)ceil_div(num_rows * kWave, kBlock)),
                        dim3(kBlock), 0, s, row_ptr, col_idx, (int)num_rows, rps, (int)nb,
                        (int)bucket_shift, keys, row_of);
@@ -298,8 +301,8 @@ extern "C" int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx,
     MAXK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_out, ids, eid,
                                                 (int)num_e, 0, key_bits(nt), s));
     hipLaunchKernelGGL(pull_gather_kernel, dim3((unsigned)ceil_div(num_e, kBlock)), dim3(kBlock),
-                       0, s, eid, row_of, col_idx, edge_val, num_e, (int)bucket_shift, ent_row,
-                       ent_w, ent_dst);
+                       0, s, eid, row_of, col_idx, edge_val, num_e, (int)bucket_shift, rps,
+                       reinterpret_cast<uint2 *>(ent));
     MAXK_LAUNCHED("pull_gather_kernel");
     hipLaunchKernelGGL(tile_ptr_kernel, dim3((unsigned)ceil_div(num_e + 1, kBlock)), dim3(kBlock),
                        0, s, keys_out, num_e, (int)nt, tile_ptr);

@@ -311,11 +311,11 @@ _PULL_CACHE: dict = {}
 
 def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_cols: int,
               k: int, dim: int = 256, slices: Optional[int] = None, cache: bool = True):
-    """(tile_ptr int32 [S*nb+1], ent_row int32 [E], ent_w f32 [E], ent_dst uint16 [E], shift,
-    S) of a CSR graph and its edge values for the pull backward at width k: rows cut into S
-    slices (default maxk_pull_slices: ~3.5 MiB of G rows each), columns into buckets of
-    2^shift; per tile (slice, bucket) the edges in CSR order with their source row, weight
-    and column inside the bucket.  Built on the GPU (one stable radix sort); cached per
+    """(tile_ptr int32 [S*nb+1], ent int32 [E, 2], shift, S) of a CSR graph and its edge
+    values for the pull backward at width k: rows cut into S slices (default
+    maxk_pull_slices: ~3.5 MiB of G rows each), columns into buckets of 2^shift; per tile
+    (slice, bucket) the edges in CSR order, each {row in its slice | column in its bucket
+    << 16, weight bits}.  Built on the GPU (one stable radix sort); cached per
     (indices, values) tensor objects and their version counters -- the weights are copied
     into the plan, so a plan serves the values it was built from."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
@@ -338,17 +338,14 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     E = indices.numel()
     nb = int(L.maxk_bucket_count(num_cols, shift))
     tptr = torch.empty(S * nb + 1, dtype=torch.int32, device=dev)
-    erow = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
-    ew = torch.empty(max(E, 1), dtype=torch.float32, device=dev)[:E]
-    edst = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
+    ent = torch.empty(max(E, 1), 2, dtype=torch.int32, device=dev)[:E]
     ws = torch.empty(max(1, L.maxk_pull_plan_workspace_size(num_rows, num_cols, E, shift, S)),
                      dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev):
         _capi.check(L.maxk_pull_plan(_ptr(indptr), _ptr(indices), _ptr(values), num_rows,
-                                     num_cols, E, shift, S, _ptr(tptr), _ptr(erow), _ptr(ew),
-                                     _ptr(edst), _ptr(ws), ws.numel(), _stream(dev)),
-                    "maxk_pull_plan")
-    plan = (tptr, erow, ew, edst, shift, S)
+                                     num_cols, E, shift, S, _ptr(tptr), _ptr(ent), _ptr(ws),
+                                     ws.numel(), _stream(dev)), "maxk_pull_plan")
+    plan = (tptr, ent, shift, S)
     if cache:
         if key not in _PULL_CACHE:
             weakref.finalize(indices, _PULL_CACHE.pop, key, None)
@@ -377,7 +374,7 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
             shift = int(_lib().maxk_bucket_shift(int(k)))
             rows = num_rows if num_rows else num_cols
             if num_e * (1 << shift) >= rows * num_cols // 2:
-                mode = "pull"
+                mode = "pull" if rows <= 256 * 65536 else "bucket"
     if mode in ("bucket", "pull") and k % 4 != 0:
         raise RuntimeError(f"backward mode {mode!r} needs k % 4 == 0, got k={k}")
     if mode == "pull" and dim is not None and dim % 4 != 0:
@@ -445,15 +442,15 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     E = indices.numel()
     mode = _bwd_mode(mode, k, E, num_cols, num_rows, D)
     if mode == "pull":
-        tptr, erow, ew, edst, shift, S = (plan if plan is not None else
-                                          pull_plan(indptr, indices, values, num_cols, k, D))
+        tptr, ent, shift, S = (plan if plan is not None else
+                               pull_plan(indptr, indices, values, num_cols, k, D))
         ws_bytes = L.maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, D, k, S)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         with torch.cuda.device(dev):
             _capi.check(L.maxk_sspmm_backward_pull(
-                _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tptr), _ptr(erow),
-                _ptr(ew), _ptr(edst), shift, S, _ptr(out), num_rows, num_cols, E, D, k,
-                _ptr(ws), ws.numel(), _stream(dev)), "maxk_sspmm_backward_pull")
+                _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tptr), _ptr(ent), shift,
+                S, _ptr(out), num_rows, num_cols, E, D, k, _ptr(ws), ws.numel(), _stream(dev)),
+                "maxk_sspmm_backward_pull")
         return out
     if mode == "bucket":
         bptr, beid, bdst, shift = plan if plan is not None else bucket_plan(indices, num_cols, k)

@@ -48,13 +48,13 @@ SIGNATURES = {
     "maxk_bucket_plan_workspace_size": (_sz, [_i64, _i64]),
     "maxk_bucket_plan": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "maxk_sspmm_backward_pull_workspace_size": (_sz, [_i64, _i64, _i32, _i32, _i32]),
-    "maxk_sspmm_backward_pull": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i32, _i32, _p, _i64,
-                                                _i64, _i64, _i32, _i32, _p, _sz, _p]),
+    "maxk_sspmm_backward_pull": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _p, _i64, _i64,
+                                                _i64, _i32, _i32, _p, _sz, _p]),
     "maxk_pull_shift": (ctypes.c_int, [_i32]),
     "maxk_pull_slices": (ctypes.c_int, [_i64, _i32]),
     "maxk_pull_plan_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32]),
-    "maxk_pull_plan": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _p,
-                                      _p, _sz, _p]),
+    "maxk_pull_plan": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _sz,
+                                      _p]),
     "maxk_topk_cbsr": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_u8": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_cbsr_scatter_dense": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),

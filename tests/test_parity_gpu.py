@@ -118,18 +118,18 @@ def test_pull_plan(mk, cuda, path):
     col = z["col_idx"].astype(np.int64)
     rows = np.repeat(np.arange(V), np.diff(z["row_ptr"]))
     for k, S in ((4, 1), (16, 3), (16, 50)):
-        tptr, erow, ew, edst, shift, s_ = mk.pull_plan(T(z["row_ptr"], cuda), T(z["col_idx"], cuda),
-                                                       T(z["val"], cuda), V, k, slices=S,
-                                                       cache=False)
+        tptr, ent, shift, s_ = mk.pull_plan(T(z["row_ptr"], cuda), T(z["col_idx"], cuda),
+                                            T(z["val"], cuda), V, k, slices=S, cache=False)
         assert s_ == S and shift == mk._lib().maxk_pull_shift(k)
         nb = (V + (1 << shift) - 1) >> shift
         rps = -(-V // S)
         key = (rows // rps) * nb + (col >> shift)
         order = np.argsort(key, kind="stable")
         assert np.array_equal(tptr.cpu().numpy(), np.searchsorted(key[order], np.arange(S * nb + 1)))
-        assert np.array_equal(erow.cpu().numpy(), rows[order])
-        assert np.array_equal(ew.cpu().numpy(), z["val"][order])
-        assert np.array_equal(edst.cpu().numpy().astype(np.int64), col[order] & ((1 << shift) - 1))
+        e = ent.cpu().numpy().view(np.uint32)
+        assert np.array_equal(e[:, 0] & 0xffff, rows[order] % rps)
+        assert np.array_equal(e[:, 0] >> 16, col[order] & ((1 << shift) - 1))
+        assert np.array_equal(e[:, 1].view(np.float32), z["val"][order])
 
 
 def test_pull_plan_follows_values(mk, cuda):
@@ -184,7 +184,7 @@ def test_bucket_backward_many_parts(mk, cuda, k, mode):
         tc, vc = T(col, cuda), T(val, cuda)
         for S in (1, 7, 100):
             plan = mk.pull_plan(T(row_ptr, cuda), tc, vc, V, k, D, slices=S, cache=False)
-            assert plan[5] == S
+            assert plan[3] == S
             gs = mk.sspmm_backward(T(row_ptr, cuda), tc, vc, T(g, cuda), T(ci, cuda),
                                    row_div=T(div, cuda), mode="pull", plan=plan)
             close(gs, go)

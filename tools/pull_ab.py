@@ -59,5 +59,5 @@ for S in a.slices:
     plan = mk.pull_plan(row_ptr, col, val, V, k, D, slices=S or None, cache=False)
     got = run("pull", plan)
     err = ((got - ref).abs().max() / ref.abs().max()).item()
-    print(f"pull S={plan[5]:4d}: {t(lambda: run('pull', plan)):.3f} ms  max rel err vs bucket "
+    print(f"pull S={plan[3]:4d}: {t(lambda: run('pull', plan)):.3f} ms  max rel err vs bucket "
           f"{err:.3e}")
