@@ -6,7 +6,7 @@
 //
 // Every edge needs the k values of its source row's G picked by its destination's
 // selectors, summed per destination c.  Four forms of that sum:
-//  * pull (maxk_sspmm_backward_pull, the default for k % 4 == 0, k <= 16 on dense graphs):
+//  * pull (maxk_sspmm_backward_pull, the default for k % 4 == 0 on dense graphs):
 //    per tile (row slice, destination bucket) the edges' values are gathered straight from
 //    G / row_div into an fp64 LDS accumulator; no per-edge contribution rows
 //    (pull_tile_kernel below).

@@ -361,20 +361,24 @@ BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic")
 def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0,
               num_rows: Optional[int] = None, dim: Optional[int] = None) -> str:
     """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) picks "pull"
-    where it measured faster than "csc": k % 4 == 0, k <= 16 (the fp64 LDS adds grow with k)
-    and at least ~1/2 edge per (source row, bucket) on average (Reddit k=16: 2.2;
-    ogbn-products: 0.02), and dim % 4 == 0 when dim is given; "bucket" (the two-phase form
-    with the same accumulator) stays selectable."""
+    where it measured faster than "csc": k % 4 == 0, dim % 4 == 0 when dim is given, and at
+    least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(k) columns) on average
+    (Reddit k=16: 2.2, k=64: 0.54; ogbn-proteins k=64: 1.2; ogbn-products: 0.02); for more
+    than 256 x 65536 rows "bucket" (k <= 16) stands in.  "bucket" (two-phase with the same
+    fp64 accumulator) stays selectable."""
     mode = mode or os.environ.get("MAXK_BWD_MODE", "auto")
     if mode not in BWD_MODES:
         raise RuntimeError(f"backward mode must be one of {BWD_MODES}, got {mode!r}")
     if mode == "auto":
         mode = "csc"
-        if k % 4 == 0 and k <= 16 and num_cols > 0 and (dim is None or dim % 4 == 0):
+        if k % 4 == 0 and num_cols > 0 and (dim is None or dim % 4 == 0):
             shift = int(_lib().maxk_bucket_shift(int(k)))
             rows = num_rows if num_rows else num_cols
             if num_e * (1 << shift) >= rows * num_cols // 2:
-                mode = "pull" if rows <= 256 * 65536 else "bucket"
+                if rows <= 256 * 65536:
+                    mode = "pull"
+                elif k <= 16:
+                    mode = "bucket"
     if mode in ("bucket", "pull") and k % 4 != 0:
         raise RuntimeError(f"backward mode {mode!r} needs k % 4 == 0, got k={k}")
     if mode == "pull" and dim is not None and dim % 4 != 0:

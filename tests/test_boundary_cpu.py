@@ -102,9 +102,9 @@ def test_autograd_surface_no_cpu_fallback():
 
 
 def test_backward_mode_resolution():
-    """mode "auto": pull for k % 4 == 0, k <= 16, dim % 4 == 0 and >= 1/2 edge per (source
-    row, bucket), else csc; "bucket" / "pull" refuse k % 4 != 0, "pull" dim % 4 != 0;
-    unknown modes are rejected (no silent fallback)."""
+    """mode "auto": pull for k % 4 == 0, dim % 4 == 0 and >= 1/2 edge per (source row,
+    bucket), else csc; "bucket" / "pull" refuse k % 4 != 0, "pull" dim % 4 != 0; unknown
+    modes are rejected (no silent fallback)."""
     import maxk_cuda_kernels as mk
     reddit = dict(num_e=114_615_891, num_cols=232_965, num_rows=232_965)
     products = dict(num_e=123_718_280, num_cols=2_449_029, num_rows=2_449_029)
@@ -112,7 +112,11 @@ def test_backward_mode_resolution():
     assert mk._bwd_mode("auto", 16, **reddit, dim=256) == "pull"
     assert mk._bwd_mode("auto", 16, **reddit, dim=9) == "csc"
     assert mk._bwd_mode("auto", 8, **reddit) == "pull"
-    assert mk._bwd_mode("auto", 32, **reddit) == "csc"
+    assert mk._bwd_mode("auto", 32, **reddit) == "pull"
+    assert mk._bwd_mode("auto", 64, **reddit) == "pull"
+    proteins = dict(num_e=79_122_504, num_cols=132_534, num_rows=132_534)
+    assert mk._bwd_mode("auto", 64, **proteins) == "pull"
+    assert mk._bwd_mode("auto", 32, **products) == "csc"
     assert mk._bwd_mode("auto", 12, **reddit) == "pull"
     assert mk._bwd_mode("auto", 10, **reddit) == "csc"
     assert mk._bwd_mode("auto", 16, **products) == "csc"

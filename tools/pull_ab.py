@@ -18,6 +18,7 @@ ap.add_argument("--graph", default="reddit")
 ap.add_argument("--k", type=int, default=16)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--slices", type=int, nargs="*", default=[0, 32, 128])
+ap.add_argument("--csc", action="store_true", help="also time the csc two-phase form")
 a = ap.parse_args()
 P = maxk_graph.PRESETS[a.graph]
 dev = torch.device("cuda")
@@ -55,6 +56,10 @@ def run(mode, plan):
 
 ref = run("bucket", bplan).clone()
 print(f"{a.graph} k={k} V={V} E={E}: bucket (two-phase) {t(lambda: run('bucket', bplan)):.3f} ms")
+if a.csc:
+    cplan = mk.transpose_plan(col, V)
+    print(f"csc (two-phase) {t(lambda: run('csc', cplan)):.3f} ms")
+    del cplan
 for S in a.slices:
     plan = mk.pull_plan(row_ptr, col, val, V, k, D, slices=S or None, cache=False)
     got = run("pull", plan)
