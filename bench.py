@@ -129,7 +129,24 @@ def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
     out["multi_thread"] = {"value": round(2 * E / (t2 - t0) / 1e9, 6), "cores": nt,
                            "sample": f"whole graph, {nt} OpenMP threads (backward in pull form); "
                                      f"fwd {t1 - t0:.2f}s, bwd {t2 - t1:.2f}s"}
+    out["host"] = host_info()
     return out
+
+
+def host_info():
+    """The host the CPU baselines ran on (record nproc and the CPU model)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "torch_threads": torch.get_num_threads()}
 
 
 def cpu_spmm_baselines(row_ptr, col, val, dense, target_s=6.0):
