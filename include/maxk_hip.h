@@ -171,10 +171,10 @@ int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
  * ceil(num_rows/slices) <= 65536 rows, nb = maxk_bucket_count(num_cols, shift)); per tile,
  * in CSR order, ent[2*num_e] = one uint32 pair per edge: {row - first row of its slice |
  * (column - first column of its bucket) << 16, bits of edge_val}.  maxk_pull_shift(k) is
- * the bucket shift to use; maxk_pull_slices(num_rows, dim_origin) the default slice count
+ * the bucket shift to use; maxk_pull_slices(num_rows, dim_origin, dim_k) the default slice count
  * (about 3.5 MiB of G rows per slice, at least num_rows/65536, 1..256). */
 int maxk_pull_shift(int32_t dim_k);
-int maxk_pull_slices(int64_t num_rows, int32_t dim_origin);
+int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
                                      int32_t bucket_shift, int32_t slices);
 int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,

@@ -240,9 +240,13 @@ extern "C" int maxk_pull_shift(int32_t dim_k) {
     return s < 0 ? s : (s > MAXK_PULL_SHIFT_DELTA ? s - MAXK_PULL_SHIFT_DELTA : 0);
 }
 
-extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin) {
+// ~3.5 MiB of G rows per slice up to k = 16, k/16 times that above: the S tile partials
+// (S x num_cols x k floats, written and read once) grow with k, the gather locality does not
+// (Reddit: S = 66 / 33 / 16 best at k = 16 / 32 / 64, profiles/r01/tune/pull_slices_k.txt).
+extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
-    int64_t s = (num_rows * dim_origin * 4 + maxk::kPullSliceBytes - 1) / maxk::kPullSliceBytes;
+    const int64_t per = maxk::kPullSliceBytes * (dim_k > 16 ? dim_k / 16 : 1);
+    int64_t s = (num_rows * dim_origin * 4 + per - 1) / per;
     const int64_t lo = (num_rows + 65535) / 65536;  // rows within a slice fit 16 bits
     s = s < lo ? lo : s;
     return (int)(s < 1 ? 1 : (s > 256 ? 256 : s));
