@@ -117,6 +117,12 @@ def test_backward_mode_resolution():
     proteins = dict(num_e=79_122_504, num_cols=132_534, num_rows=132_534)
     assert mk._bwd_mode("auto", 64, **proteins) == "pull"
     assert mk._bwd_mode("auto", 32, **products) == "csc"
+    assert mk._bwd_mode("auto", 16, **products, dim=256) == "csc"
+    # a small gradient (Flickr, 23 MB) stays cache-resident: pull however sparse the graph
+    flickr = dict(num_e=989_006, num_cols=89_250, num_rows=89_250)
+    assert mk._bwd_mode("auto", 16, **flickr) == "csc"
+    assert mk._bwd_mode("auto", 16, **flickr, dim=64) == "pull"
+    assert mk._bwd_mode("auto", 10, **flickr, dim=64) == "csc"
     assert mk._bwd_mode("auto", 12, **reddit) == "pull"
     assert mk._bwd_mode("auto", 10, **reddit) == "csc"
     assert mk._bwd_mode("auto", 16, **products) == "csc"

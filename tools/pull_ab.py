@@ -19,11 +19,12 @@ ap.add_argument("--k", type=int, default=16)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--slices", type=int, nargs="*", default=[0, 32, 128])
 ap.add_argument("--csc", action="store_true", help="also time the csc two-phase form")
+ap.add_argument("--dim", type=int, default=None, help="feature width (default: the preset's)")
 a = ap.parse_args()
 P = maxk_graph.PRESETS[a.graph]
 dev = torch.device("cuda")
 row_ptr, col = maxk_graph.make_graph(P["V"], P["E"], P["alpha"], P["i0"], 1, dev)
-V, E, D, k = row_ptr.numel() - 1, col.numel(), 256, a.k
+V, E, D, k = row_ptr.numel() - 1, col.numel(), a.dim or P["D"], a.k
 g = torch.Generator(device=dev).manual_seed(123)
 val = torch.rand(E, device=dev, generator=g)
 x = torch.rand(V, D, device=dev, generator=g)
