@@ -54,6 +54,9 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif
+#ifndef MAXK_SCATTER_ROWS4  // dense scatter: four rows per wave
+#define MAXK_SCATTER_ROWS4 1
+#endif
 #ifndef MAXK_TOPK_BLOCKS  // grid cap of the grid-stride top-k (rows per wave grow past it)
 #define MAXK_TOPK_BLOCKS 16384
 #endif

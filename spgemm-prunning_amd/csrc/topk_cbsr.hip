@@ -443,6 +443,52 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
 // optional).  One wave per row, grid-stride: one workgroup per 4 rows would be bound by
 // workgroup dispatch on large graphs.  A row's reads all land in LDS before its stores, so
 // dense may alias add (in-place MaxK gradient).
+#if MAXK_SCATTER_ROWS4
+// Four rows per wave, 16 lanes per row for the k (index, value) pairs; the four 1 KB rows are
+// then stored one per wave instruction (16 B per lane).  One row per wave left each wave a
+// chain of dependent byte loads, an LDS round trip and a store per row.
+__global__ __launch_bounds__(kBlock) void cbsr_scatter_dense_kernel(
+    const float *__restrict__ val, const uint8_t *__restrict__ idx, const float *add,
+    float *dense, int num_rows, int D, int k) {
+    __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][4][kMaxDim];
+    const int wid = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int sub = lane >> 4, sl = lane & 15;
+    float(*buf)[kMaxDim] = lds[wid];
+    const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock * 4;
+    for (int64_t g0 = ((int64_t)blockIdx.x * kWavesPerBlock + wid) * 4; g0 < num_rows;
+         g0 += stride) {
+        const int64_t row = g0 + sub;
+        float4 *b4 = reinterpret_cast<float4 *>(&buf[sub][sl * 16]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        wave_lds_fence();
+        if (row < num_rows) {
+            for (int l = sl; l < k; l += 16) {
+                const int j = idx[row * k + l];
+                float x = val ? val[row * k + l] : 0.f;
+                if (add) x += add[row * D + j];
+                buf[sub][j] = x;
+            }
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+            const int64_t r = g0 + rr;
+            if (r >= num_rows) break;
+            float *dst = dense + r * D;
+            if ((D & 3) == 0) {
+                for (int j = lane * 4; j < D; j += kWave * 4)
+                    *reinterpret_cast<float4 *>(&dst[j]) =
+                        *reinterpret_cast<const float4 *>(&buf[rr][j]);
+            } else {
+                for (int j = lane; j < D; j += kWave) dst[j] = buf[rr][j];
+            }
+        }
+        wave_lds_fence();
+    }
+}
+#else
 __global__ __launch_bounds__(kBlock) void cbsr_scatter_dense_kernel(
     const float *__restrict__ val, const uint8_t *__restrict__ idx, const float *add,
     float *dense, int num_rows, int D, int k) {
@@ -471,6 +517,7 @@ __global__ __launch_bounds__(kBlock) void cbsr_scatter_dense_kernel(
         wave_lds_fence();
     }
 }
+#endif
 
 template <typename T>
 int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, T *dense,
@@ -548,7 +595,7 @@ int scatter_launch(const float *val, const uint8_t *idx, const float *add, float
     MAXK_REQUIRE(dim_k >= 1 && dim_k <= dim_origin, "dim_k must be in [1,dim_origin]");
     if (num_rows == 0) return MAXK_OK;
     MAXK_REQUIRE(idx && dense, "pointers must not be NULL");
-    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
+    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock * (MAXK_SCATTER_ROWS4 ? 4 : 1));
     const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
     hipLaunchKernelGGL(cbsr_scatter_dense_kernel, grid, dim3(kBlock), 0, as_stream(stream), val,
                        idx, add, dense, (int)num_rows, dim_origin, dim_k);
