@@ -150,7 +150,7 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
  * Backward, pull form (no contribution rows): the same result as maxk_sspmm_backward,
  * summed per tile (row slice x destination bucket of 2^shift columns) from G / row_div
  * gathered directly, fp64 LDS accumulation, then the slices of a bucket added in slice
- * order (deterministic).  Needs dim_k % 4 == 0, dim_origin % 4 == 0 and
+ * order (deterministic).  Needs dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and
  * bucket_shift == maxk_bucket_shift(dim_k), the pull plan of the graph built with the same
  * shift, slices and edge_val (maxk_pull_plan), and a workspace of
  * maxk_sspmm_backward_pull_workspace_size(...) bytes (G / row_div plus slices x

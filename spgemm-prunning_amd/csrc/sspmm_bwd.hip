@@ -574,7 +574,7 @@ __global__ __launch_bounds__(kBlock) void gprime_kernel(const float *__restrict_
 // accumulator, SEL_LDS), four gathers and four LDS adds; 64/LR entries per wave
 // instruction, U instructions per wave step, the next step's entries prefetched.
 // Entry = {row within the slice | column within the bucket << 16, weight bits}.
-template <int LR, int U, bool SEL_LDS>
+template <int LR, int U, bool SEL_LDS, int VPL>
 __global__ __launch_bounds__(1024) void pull_tile_kernel(
     const float *__restrict__ Gp, const uint8_t *__restrict__ cbsr_idx,
     const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
@@ -586,20 +586,22 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
     const int tid = threadIdx.x;
     const int lane = lane_id(), w = tid / kWave;
     const int g = lane / LR, q = lane % LR;
-    const int kq = k >> 2;
-    const bool qok = q < kq;
+    const bool qok = q < k / VPL;
     const int ks = k + 1;
     const int t = blockIdx.x;
     const int j = t % n_buckets;
     const float *__restrict__ Gs = Gp + (size_t)(t / n_buckets) * rows_per_slice * D;
     const int s0 = tile_ptr[t], s1 = tile_ptr[t + 1];
     const int64_t c0 = (int64_t)j << shift;
-    const uint32_t *__restrict__ selg = reinterpret_cast<const uint32_t *>(cbsr_idx + c0 * k);
-    uint32_t *sel_lds = reinterpret_cast<uint32_t *>(acc + (ks << shift));
+    const uint8_t *__restrict__ selg = cbsr_idx + c0 * k;
+    uint8_t *sel_lds = reinterpret_cast<uint8_t *>(acc + (ks << shift));
     for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
     if (SEL_LDS) {
         const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
-        for (int i = tid; i < rows * kq; i += 1024) sel_lds[i] = selg[i];
+        const int nb = rows * k;  // c0 * k is a multiple of 4 (shift >= 2)
+        for (int i = tid; i < nb / 4; i += 1024)
+            reinterpret_cast<uint32_t *>(sel_lds)[i] = reinterpret_cast<const uint32_t *>(selg)[i];
+        for (int i = (nb & ~3) + tid; i < nb; i += 1024) sel_lds[i] = selg[i];
     }
     __syncthreads();
     int base = s0 + w * STEP;
@@ -621,24 +623,26 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
         for (int u = 0; u < U; ++u) {
             const uint32_t key = en[u].x;
             dc[u] = (key >> 16) == 0xffffu ? -1 : (int)(key >> 16);
-            const int si = (dc[u] < 0 ? 0 : dc[u]) * kq + (qok ? q : 0);
-            sv[u] = SEL_LDS ? sel_lds[si] : selg[si];
+            // VPL (4 or 1) consecutive selectors of the entry's destination, lane q's share
+            const int bo = (dc[u] < 0 ? 0 : dc[u]) * k + (qok ? q : 0) * VPL;
+            const uint8_t *sb8 = SEL_LDS ? sel_lds : selg;
+            sv[u] = VPL == 4 ? *reinterpret_cast<const uint32_t *>(sb8 + bo) : (uint32_t)sb8[bo];
         }
-        float v[U][4];
+        float v[U][VPL];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float *gr = Gs + (en[u].x & 0xffffu) * (uint32_t)D;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[u][i] = gr[(sv[u] >> (8 * i)) & 255u];
+            for (int i = 0; i < VPL; ++i) v[u][i] = gr[(sv[u] >> (8 * i)) & 255u];
             wc[u] = __uint_as_float(en[u].y);
         }
         if (base + 16 * STEP < s1) load_ids(base + 16 * STEP);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (dc[u] >= 0 && qok) {
-                double *a = &acc[dc[u] * ks + 4 * q];
+                double *a = &acc[dc[u] * ks + VPL * q];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) atomicAdd(a + i, (double)(wc[u] * v[u][i]));
+                for (int i = 0; i < VPL; ++i) atomicAdd(a + i, (double)(wc[u] * v[u][i]));
             }
         }
     }
@@ -656,9 +660,19 @@ __global__ __launch_bounds__(kBlock) void pull_reduce_kernel(const float *__rest
     const int64_t c0 = (int64_t)j << shift;
     const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
     const int i = blockIdx.y * kBlock + threadIdx.x;
-    if (i >= rows * k / 4) return;
+    const int nf = rows * k;  // floats of this bucket; tiles and c0 * k are 16-B aligned
+    if (i * 4 >= nf) return;
     const size_t n4 = ((size_t)k << shift) / 4;
     const float4 *to = reinterpret_cast<const float4 *>(tile_out);
+    if (i * 4 + 4 > nf) {  // k % 4 != 0: the bucket's last 1..3 floats
+        const int f0 = i * 4;
+        for (int f = f0; f < nf; ++f) {
+            float a = tile_out[(size_t)j * n4 * 4 + f];
+            for (int s = 1; s < slices; ++s) a += tile_out[((size_t)s * n_buckets + j) * n4 * 4 + f];
+            grad_cbsr[c0 * k + f] = a;
+        }
+        return;
+    }
     float4 a = to[(size_t)j * n4 + i];
     for (int s = 1; s < slices; ++s) {
         const float4 b = to[((size_t)s * n_buckets + j) * n4 + i];
@@ -1022,7 +1036,8 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
                                         void *stream) {
     clear_error();
     if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, 0)) return rc;
-    MAXK_REQUIRE(dim_k % 4 == 0, "pull backward needs dim_k %% 4 == 0, got %d", dim_k);
+    MAXK_REQUIRE(dim_k % 4 == 0 || dim_k <= 64,
+                 "pull backward needs dim_k %% 4 == 0 or dim_k <= 64, got %d", dim_k);
     MAXK_REQUIRE(dim_origin % 4 == 0, "pull backward needs dim_origin %% 4 == 0, got %d",
                  dim_origin);
     MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= maxk_bucket_shift(dim_k) &&
@@ -1061,10 +1076,17 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     const bool sel_lds = acc_b + sel_b <= kPullLdsBytes;
     const size_t lds = acc_b + (sel_lds ? sel_b : 0);
     const uint2 *ent2 = reinterpret_cast<const uint2 *>(ent);
-    switch (lanes_per_edge(k / 4) * 2 + (sel_lds ? 1 : 0)) {
+    // four l per lane (one u32 selector read) when k % 4 == 0, else one
+    const bool v4 = k % 4 == 0;
+    switch (lanes_per_edge(v4 ? k / 4 : k) * 4 + (sel_lds ? 1 : 0) + (v4 ? 2 : 0)) {
 #define MAXK_CASE(LRV, SL)                                                                    \
-    case LRV * 2 + SL:                                                                        \
-        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL>), dim3(tiles), dim3(1024),  \
+    case LRV * 4 + SL + 2:                                                                    \
+        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL, 4>), dim3(tiles), dim3(1024), \
+                           lds, s, Gp, cbsr_idx, tile_ptr, ent2, tile_out, num_cols, (int)nb,  \
+                           (int)rps, dim_origin, k, bucket_shift);                            \
+        break;                                                                                \
+    case LRV * 4 + SL:                                                                        \
+        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL, 1>), dim3(tiles), dim3(1024), \
                            lds, s, Gp, cbsr_idx, tile_ptr, ent2, tile_out, num_cols, (int)nb,  \
                            (int)rps, dim_origin, k, bucket_shift);                            \
         break;
@@ -1082,7 +1104,7 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     }
     MAXK_LAUNCHED("pull_tile_kernel");
     hipLaunchKernelGGL(pull_reduce_kernel,
-                       dim3((unsigned)nb, (unsigned)ceil_div(((int64_t)k << bucket_shift) / 4, kBlock)),
+                       dim3((unsigned)nb, (unsigned)ceil_div(ceil_div((int64_t)k << bucket_shift, 4), kBlock)),
                        dim3(kBlock), 0, s, tile_out, grad_cbsr, num_cols, (int)nb, slices, k,
                        bucket_shift);
     MAXK_LAUNCHED("pull_reduce_kernel");

@@ -362,7 +362,8 @@ BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic")
 def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0,
               num_rows: Optional[int] = None, dim: Optional[int] = None) -> str:
     """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) picks "pull"
-    where it measured faster than "csc": k % 4 == 0, dim % 4 == 0 when dim is given, and at
+    where it measured faster than "csc": k % 4 == 0 or k <= 64, dim % 4 == 0 when dim is
+    given, and at
     least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(k) columns) on average
     (Reddit k=16: 2.2, k=64: 0.54; ogbn-proteins k=64: 1.2; ogbn-products: 0.02), or a
     gradient G of at most 64 MiB (num_rows x dim x 4 B; Flickr: 23 MB, 0.05 vs 0.13 ms), which
@@ -374,17 +375,19 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
         raise RuntimeError(f"backward mode must be one of {BWD_MODES}, got {mode!r}")
     if mode == "auto":
         mode = "csc"
-        if k % 4 == 0 and num_cols > 0 and (dim is None or dim % 4 == 0):
+        if (k % 4 == 0 or k <= 64) and num_cols > 0 and (dim is None or dim % 4 == 0):
             shift = int(_lib().maxk_bucket_shift(int(k)))
             rows = num_rows if num_rows else num_cols
             dense = num_e * (1 << shift) >= rows * num_cols // 2
             small = dim is not None and rows * dim * 4 <= (64 << 20)
             if (dense or small) and rows <= 256 * 65536:
                 mode = "pull"
-            elif dense and k <= 16:
+            elif dense and k <= 16 and k % 4 == 0:
                 mode = "bucket"
-    if mode in ("bucket", "pull") and k % 4 != 0:
-        raise RuntimeError(f"backward mode {mode!r} needs k % 4 == 0, got k={k}")
+    if mode == "bucket" and k % 4 != 0:
+        raise RuntimeError(f"backward mode 'bucket' needs k % 4 == 0, got k={k}")
+    if mode == "pull" and k % 4 != 0 and k > 64:
+        raise RuntimeError(f"backward mode 'pull' needs k % 4 == 0 or k <= 64, got k={k}")
     if mode == "pull" and dim is not None and dim % 4 != 0:
         raise RuntimeError(f"backward mode 'pull' needs dim_origin % 4 == 0, got {dim}")
     return mode

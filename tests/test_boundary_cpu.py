@@ -102,9 +102,9 @@ def test_autograd_surface_no_cpu_fallback():
 
 
 def test_backward_mode_resolution():
-    """mode "auto": pull for k % 4 == 0, dim % 4 == 0 and >= 1/2 edge per (source row,
-    bucket), else csc; "bucket" / "pull" refuse k % 4 != 0, "pull" dim % 4 != 0; unknown
-    modes are rejected (no silent fallback)."""
+    """mode "auto": pull for k % 4 == 0 or k <= 64, dim % 4 == 0 and >= 1/2 edge per (source
+    row, bucket) or a small G, else csc; "bucket" refuses k % 4 != 0, "pull" k % 4 != 0 above
+    64 and dim % 4 != 0; unknown modes are rejected (no silent fallback)."""
     import maxk_cuda_kernels as mk
     reddit = dict(num_e=114_615_891, num_cols=232_965, num_rows=232_965)
     products = dict(num_e=123_718_280, num_cols=2_449_029, num_rows=2_449_029)
@@ -122,9 +122,11 @@ def test_backward_mode_resolution():
     flickr = dict(num_e=989_006, num_cols=89_250, num_rows=89_250)
     assert mk._bwd_mode("auto", 16, **flickr) == "csc"
     assert mk._bwd_mode("auto", 16, **flickr, dim=64) == "pull"
-    assert mk._bwd_mode("auto", 10, **flickr, dim=64) == "csc"
+    assert mk._bwd_mode("auto", 10, **flickr, dim=64) == "pull"
+    assert mk._bwd_mode("auto", 16, **flickr, dim=9) == "csc"
     assert mk._bwd_mode("auto", 12, **reddit) == "pull"
-    assert mk._bwd_mode("auto", 10, **reddit) == "csc"
+    assert mk._bwd_mode("auto", 10, **reddit) == "pull"  # one l per lane below k % 4
+    assert mk._bwd_mode("auto", 66, **reddit) == "csc"
     assert mk._bwd_mode("auto", 16, **products) == "csc"
     # a shard of 1/8 of the rows keeps Reddit's per-row degree: still the pull form
     assert mk._bwd_mode("auto", 16, num_e=14_326_986, num_cols=232_968, num_rows=29_121) == "pull"
@@ -134,7 +136,7 @@ def test_backward_mode_resolution():
     with pytest.raises(RuntimeError):
         mk._bwd_mode("bucket", 6, **reddit)
     with pytest.raises(RuntimeError):
-        mk._bwd_mode("pull", 6, **reddit)
+        mk._bwd_mode("pull", 66, **reddit)
     with pytest.raises(RuntimeError):
         mk._bwd_mode("pull", 16, **reddit, dim=9)
     with pytest.raises(RuntimeError):
