@@ -606,16 +606,42 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
     __syncthreads();
     int base = s0 + w * STEP;
     uint2 en[U];
+    // kShfl: 8-B loads with one entry per lane fetch the step's STEP entries (NL = STEP / 64
+    // loads); each lane group then takes its entry from the loading lane with ds_bpermute:
+    // NL memory instructions per step for the entries instead of U (the texture addresser,
+    // not LDS, is the busy unit; Reddit k=8 / 16 / 32: -3.5 / -5.8 / -5.3 %).  With more than
+    // 8 lanes per entry the two shuffles per instruction outweigh the loads saved (k=64 +4 %).
+    constexpr bool kShfl = MAXK_PULL_SHFL && LR <= 8;
+    constexpr int NL = (STEP + kWave - 1) / kWave;
+    uint2 my[NL];
     auto load_ids = [&](int b) {
+        if constexpr (kShfl) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = b + u * EPI + g;
-            en[u] = ent[e < s1 ? e : s1 - 1];
-            if (e >= s1) en[u].x = 0xffff0000u;  // no entry: row 0 (a valid gather), column 0xffff
+            for (int m = 0; m < NL; ++m) {
+                const int e = b + m * kWave + lane;
+                my[m] = ent[e < s1 ? e : s1 - 1];
+                if (e >= s1 || m * kWave + lane >= STEP) my[m].x = 0xffff0000u;  // no entry
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = b + u * EPI + g;
+                en[u] = ent[e < s1 ? e : s1 - 1];
+                if (e >= s1) en[u].x = 0xffff0000u;  // no entry: row 0 (a valid gather), column 0xffff
+            }
         }
     };
     if (base < s1) load_ids(base);
     for (; base < s1; base += 16 * STEP) {
+        if constexpr (kShfl) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int m = (u * EPI) / kWave;  // compile-time after unrolling
+                const int src = (u * EPI + g - m * kWave) * 4;
+                en[u].x = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)my[m].x);
+                en[u].y = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)my[m].y);
+            }
+        }
         uint32_t sv[U];
         int dc[U];
         float wc[U];
