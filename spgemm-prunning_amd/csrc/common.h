@@ -51,6 +51,9 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_SHFL  // pull: the step's entries by one load + lane shuffles
 #define MAXK_PULL_SHFL 1
 #endif
+#ifndef MAXK_PULL_F4_FLUSH  // pull: tile partials stored 16 B per lane
+#define MAXK_PULL_F4_FLUSH 1
+#endif
 #ifndef MAXK_PULL_U  // pull_tile_kernel: wave instructions of entries per step
 #define MAXK_PULL_U 4
 #endif

@@ -674,7 +674,15 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
     }
     __syncthreads();
     float *o = tile_out + (size_t)t * ((size_t)k << shift);
-    for (int i = tid; i < (k << shift); i += 1024) o[i] = (float)acc[i + i / k];
+    if (MAXK_PULL_F4_FLUSH && k % 4 == 0) {  // 16-B stores: 4x fewer store instructions
+        for (int i4 = tid; i4 < (k << shift) / 4; i4 += 1024) {
+            const double *a = &acc[i4 * 4 + (i4 * 4) / k];  // 4 l of one row (k % 4 == 0)
+            reinterpret_cast<float4 *>(o)[i4] =
+                make_float4((float)a[0], (float)a[1], (float)a[2], (float)a[3]);
+        }
+    } else {
+        for (int i = tid; i < (k << shift); i += 1024) o[i] = (float)acc[i + i / k];
+    }
 }
 
 // grad_cbsr rows of bucket j = the sum of its slices' tiles, in slice order.
