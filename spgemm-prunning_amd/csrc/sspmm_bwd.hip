@@ -598,10 +598,10 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
     for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
     if (SEL_LDS) {
         const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
-        const int nb = rows * k;  // c0 * k is a multiple of 4 (shift >= 2)
-        for (int i = tid; i < nb / 4; i += 1024)
-            reinterpret_cast<uint32_t *>(sel_lds)[i] = reinterpret_cast<const uint32_t *>(selg)[i];
-        for (int i = (nb & ~3) + tid; i < nb; i += 1024) sel_lds[i] = selg[i];
+        const int nb = rows * k;  // c0 * k is a multiple of 16 (shift >= 4), as is sel_lds
+        for (int i = tid; i < nb / 16; i += 1024)
+            reinterpret_cast<uint4 *>(sel_lds)[i] = reinterpret_cast<const uint4 *>(selg)[i];
+        for (int i = (nb & ~15) + tid; i < nb; i += 1024) sel_lds[i] = selg[i];
     }
     __syncthreads();
     int base = s0 + w * STEP;
@@ -1074,9 +1074,9 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
                  "pull backward needs dim_k %% 4 == 0 or dim_k <= 64, got %d", dim_k);
     MAXK_REQUIRE(dim_origin % 4 == 0, "pull backward needs dim_origin %% 4 == 0, got %d",
                  dim_origin);
-    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= maxk_bucket_shift(dim_k) &&
+    MAXK_REQUIRE(bucket_shift >= 4 && bucket_shift <= maxk_bucket_shift(dim_k) &&
                      bucket_shift <= 15,
-                 "bucket_shift %d out of range [0, min(15, maxk_bucket_shift(%d) = %d)]",
+                 "bucket_shift %d out of range [4, min(15, maxk_bucket_shift(%d) = %d)]",
                  bucket_shift, dim_k, maxk_bucket_shift(dim_k));
     const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
     MAXK_REQUIRE(slices >= 1 && slices * nb < (1LL << 31), "slices %d out of range", slices);
