@@ -109,10 +109,10 @@ def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
                    f"of the same graph = {es} of {E} edges ({100.0 * es / E:.1f}%); "
                    f"fwd {tf:.2f}s, bwd {tb:.2f}s"),
     }
-    # the same port on the host share of cores (16 on the GPU box; OpenMP), whole graph:
-    # forward over rows, backward in its pull form over the transpose (a push needs atomics)
+    # the same port on every core this process is allotted (OpenMP), whole graph: forward over
+    # rows, backward in its pull form over the transpose (a push needs atomics)
     import maxk_cuda_kernels as mk
-    nt = min(16, os.cpu_count() or 1)
+    nt = host_cores()
     col_ptr, eid = mk.transpose_plan(col, len(rp) - 1)
     rows = torch.repeat_interleave(torch.arange(len(rp) - 1, device=col.device),
                                    torch.diff(row_ptr).long())
@@ -133,6 +133,16 @@ def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
     return out
 
 
+def host_cores() -> int:
+    """Cores this process may use: OMP_NUM_THREADS when set (the GPU box allots each GPU 16
+    of its host's CPUs and sets it to 16; nproc there shows the whole machine), else the
+    affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
 def host_info():
     """The host the CPU baselines ran on (record nproc and the CPU model)."""
     model = None
@@ -146,7 +156,8 @@ def host_info():
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
-            "torch_threads": torch.get_num_threads()}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cores_used": host_cores(), "torch_threads": torch.get_num_threads()}
 
 
 def cpu_spmm_baselines(row_ptr, col, val, dense, target_s=6.0):
@@ -198,7 +209,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=10)  # >= 10 warmup
     ap.add_argument("--graph", default="reddit", choices=sorted(maxk_graph.PRESETS))
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--dim", type=int, default=None)
@@ -380,8 +391,9 @@ def main():
 
     fwd_ms = [e[0].elapsed_time(e[1]) for e in evs]
     bwd_ms = [e[1].elapsed_time(e[2]) for e in evs]
-    fwd_avg = float(np.mean(fwd_ms))
-    bwd_avg = float(np.mean(bwd_ms))
+    # per-op launch time: the median over the timed steps; means in extra
+    fwd_avg = float(np.median(fwd_ms))
+    bwd_avg = float(np.median(bwd_ms))
     ms_per_step = 1000.0 * elapsed / args.steps
     value = 2.0 * E * args.steps / elapsed / 1e9
     B_f, B_b = alg_bytes(nl, El, D, k, n_cols)
@@ -394,8 +406,8 @@ def main():
 
     extra = {
         "fwd_ms": round(fwd_avg, 4), "bwd_ms": round(bwd_avg, 4),
-        "fwd_ms_median": round(float(np.median(fwd_ms)), 4),
-        "bwd_ms_median": round(float(np.median(bwd_ms)), 4),
+        "fwd_ms_mean": round(float(np.mean(fwd_ms)), 4),
+        "bwd_ms_mean": round(float(np.mean(bwd_ms)), 4),
         "fwd_gteps": round(El / fwd_avg / 1e6, 3), "bwd_gteps": round(El / bwd_avg / 1e6, 3),
         "fwd_alg_GBs": round(B_f / fwd_avg / 1e6, 1), "bwd_alg_GBs": round(B_b / bwd_avg / 1e6, 1),
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
@@ -423,27 +435,29 @@ def main():
         e1_.synchronize()
         extra["topk_ms"] = round(e0_.elapsed_time(e1_) / 10, 4)
         if not args.no_rocsparse:
+            # every rocSPARSE CSR algorithm; ALG_DEFAULT is the spmm_cusparse.cu:30-46
+            # equivalent, the fastest one the fair denominator
+            import maxk_kernel_test as mkt
             dense = mk.cbsr_scatter_dense(cv_all, ci_all, D)
-            plan = mk.DenseSpMMPlan(row_ptr, col, val, dense)
-            for _ in range(3):
-                plan.run()
-            torch.cuda.synchronize()
-            e0_.record()
-            for _ in range(10):
-                plan.run()
-            e1_.record()
-            e1_.synchronize()
-            rs = e0_.elapsed_time(e1_) / 10
-            err = ((plan.y - y).abs() / y.abs().clamp(min=1)).max().item()
+            t_algs, y_lib = mkt.library_spmm_times(row_ptr, col, val, dense, 5, 10)
+            rs = t_algs["default"]
+            best_alg, rs_best = mkt.best_library(t_algs)
+            err = ((y_lib - y).abs() / y.abs().clamp(min=1)).max().item()
             extra.update({"rocsparse_spmm_ms": round(rs, 4),
+                          "rocsparse_spmm_ms_best": round(rs_best, 4),
+                          "rocsparse_best_alg": best_alg,
+                          "rocsparse_spmm_ms_by_alg": {a: (None if t is None else round(t, 4))
+                                                       for a, t in t_algs.items()},
                           "speedup_fwd_vs_rocsparse": round(rs / fwd_avg, 3),
                           "speedup_bwd_vs_rocsparse": round(rs / bwd_avg, 3),
                           # the step against two library SpMMs (A X and A^T G; the symmetric
                           # synthetic graph gives A^T the same sparsity)
                           "speedup_step_vs_rocsparse": round(2 * rs / (fwd_avg + bwd_avg), 3),
+                          "speedup_fwd_vs_rocsparse_best": round(rs_best / fwd_avg, 3),
+                          "speedup_bwd_vs_rocsparse_best": round(rs_best / bwd_avg, 3),
+                          "speedup_step_vs_rocsparse_best": round(2 * rs_best / (fwd_avg + bwd_avg), 3),
                           "rocsparse_vs_maxk_max_rel_err": err})
-            plan.close()
-            del dense
+            del dense, y_lib
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

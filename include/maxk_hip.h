@@ -44,6 +44,11 @@ const char *maxk_last_error(void);
 /* Number of visible HIP devices (0 without a GPU; never fails). */
 int maxk_device_count(void);
 
+/* First 16 hex digits of the SHA-256 of the sources this library was built from
+ * (spgemm-prunning_amd/Makefile: the .hip, .cpp and .h files of csrc and this header, in
+ * C-locale path order), so a test can tell a stale binary from one built from the tree. */
+const char *maxk_source_digest(void);
+
 /* ---------------------------------------------------------------------------
  * Forward row-wise-product SpGEMM:  out = diag(1/row_div) . A . scatter(cbsr)
  *   out[r, cbsr_idx[c,l]] += edge_val[e] * cbsr_val[c,l]   (e in row r, c = col_idx[e])
@@ -150,12 +155,17 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
  * Backward, pull form (no contribution rows): the same result as maxk_sspmm_backward,
  * summed per tile (row slice x destination bucket of 2^shift columns) from G / row_div
  * gathered directly, fp64 LDS accumulation, then the slices of a bucket added in slice
- * order (deterministic).  Needs dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and
- * bucket_shift == maxk_bucket_shift(dim_k), the pull plan of the graph built with the same
- * shift, slices and edge_val (maxk_pull_plan), and a workspace of
- * maxk_sspmm_backward_pull_workspace_size(...) bytes (G / row_div plus slices x
- * num_cols x k floats of tile partials).  Replaces the same reference kernels as
- * maxk_sspmm_backward (kernels/spmm_maxk_backward.cu:15-121).
+ * order.  The fp64 tile sums make two runs agree except in rare rounding ties (bitwise
+ * repeatability: maxk_sspmm_backward_csc).  For dim_k % 4 == 0 each destination's selectors
+ * are first re-ordered by column (quantile slots, sspmm_bwd.hip pull_sel_kernel) so one
+ * gather instruction touches fewer lines of a row; the sums return to CBSR order at the
+ * end.  A selector >= dim_origin contributes 0.  Needs dim_k % 4 == 0 or dim_k <= 64,
+ * dim_origin % 4 == 0, bucket_shift in [4, min(15, maxk_bucket_shift(dim_k))], the pull
+ * plan of the graph built with the same shift, slices and edge_val (maxk_pull_plan), and a
+ * workspace of maxk_sspmm_backward_pull_workspace_size(...) bytes (G / row_div, slices x
+ * num_cols x k floats of tile partials, and 2 x num_cols x k bytes of slot-ordered
+ * selectors).  Replaces the same reference kernels as maxk_sspmm_backward
+ * (kernels/spmm_maxk_backward.cu:15-121).
  * ------------------------------------------------------------------------- */
 size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int64_t num_cols,
                                                int32_t dim_origin, int32_t dim_k, int32_t slices);
@@ -170,9 +180,10 @@ int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
  * tile_ptr[slices*nb + 1] over tiles t = s*nb + j (rows cut into `slices` slices of
  * ceil(num_rows/slices) <= 65536 rows, nb = maxk_bucket_count(num_cols, shift)); per tile,
  * in CSR order, ent[2*num_e] = one uint32 pair per edge: {row - first row of its slice |
- * (column - first column of its bucket) << 16, bits of edge_val}.  maxk_pull_shift(k) is
- * the bucket shift to use; maxk_pull_slices(num_rows, dim_origin, dim_k) the default slice count
- * (about 3.5 MiB of G rows per slice, at least num_rows/65536, 1..256). */
+ * (column - first column of its bucket) << 16, bits of edge_val}; bucket_shift in [4, 15]
+ * (the backward's 16-B selector copies need 16 | 2^shift * k).  maxk_pull_shift(k) is the
+ * bucket shift to use (at least 4); maxk_pull_slices(num_rows, dim_origin, dim_k) the default
+ * slice count (about 3.5 MiB of G rows per slice, at least num_rows/65536, 1..256). */
 int maxk_pull_shift(int32_t dim_k);
 int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,

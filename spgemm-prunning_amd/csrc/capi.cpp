@@ -22,6 +22,11 @@ void clear_error() { g_err[0] = '\0'; }
 
 extern "C" int maxk_version(void) { return 100; }
 
+#ifndef MAXK_SRC_DIGEST
+#define MAXK_SRC_DIGEST "unknown"
+#endif
+extern "C" const char *maxk_source_digest(void) { return MAXK_SRC_DIGEST; }
+
 extern "C" const char *maxk_last_error(void) { return maxk::g_err; }
 
 extern "C" int maxk_device_count(void) {

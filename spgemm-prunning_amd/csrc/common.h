@@ -57,6 +57,18 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_U  // pull_tile_kernel: wave instructions of entries per step
 #define MAXK_PULL_U 4
 #endif
+#ifndef MAXK_PULL_Q  // pull, k % 4 == 0: quantile-slot selectors + pipelined pull_q_kernel
+#define MAXK_PULL_Q 1
+#endif
+#ifndef MAXK_PULL_H  // pull_q_kernel: parts per tile (destination slots split by rank)
+#define MAXK_PULL_H 2
+#endif
+#ifndef MAXK_PULL_MIN_KP  // pull_q_kernel: fewest slots per destination a part may keep
+#define MAXK_PULL_MIN_KP 16
+#endif
+#ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
+#define MAXK_PULL_XCD 1
+#endif
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif

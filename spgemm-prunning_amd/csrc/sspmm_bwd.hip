@@ -25,6 +25,8 @@
 // Phase 1 and the csc phase 2 use the token-stream work partition of common.h (one wave
 // per item of C tokens, hub rows split, short rows batched); loads-in-flight depth per
 // launch from the average degree (pick_depth).
+#include <algorithm>
+
 #include "common.h"
 
 namespace maxk {
@@ -659,7 +661,12 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
         for (int u = 0; u < U; ++u) {
             const float *gr = Gs + (en[u].x & 0xffffu) * (uint32_t)D;
 #pragma unroll
-            for (int i = 0; i < VPL; ++i) v[u][i] = gr[(sv[u] >> (8 * i)) & 255u];
+            for (int i = 0; i < VPL; ++i) {  // a selector >= D (D < 256) contributes 0
+                const uint32_t c = (sv[u] >> (8 * i)) & 255u;
+                const bool in = c < (uint32_t)D;
+                const float x = gr[in ? c : 0u];
+                v[u][i] = in ? x : 0.0f;
+            }
             wc[u] = __uint_as_float(en[u].y);
         }
         if (base + 16 * STEP < s1) load_ids(base + 16 * STEP);
@@ -685,8 +692,235 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
     }
 }
 
-// grad_cbsr rows of bucket j = the sum of its slices' tiles, in slice order.
+// ---- pull, quantile-slot form (k % 4 == 0) ----------------------------------------------
+// The gathers of pull_tile_kernel are bound by the cache lines one wave instruction touches
+// (the texture addresser and L1 take a line per cycle, not a lane): an instruction carries
+// 64 / LR entries x LR lanes, each lane one value of its entry's source row, so the ~2
+// entries of one row in an instruction land on ~6 of the row's eight 128-B lines, four
+// instructions per step.  pull_sel_kernel therefore re-orders every destination's k
+// selectors once per call: sorted ascending, and laid out so that a lane's four bytes
+// (instructions i = 0..3) hold sorted positions i * k/4 + q.  Instruction i then gathers
+// only the i-th quarter of every row's selected columns, ~2 lines of a row instead of ~6 (a
+// model of the tile stream: 9.2 -> 5.2 distinct lines per entry at Reddit's ~2.2 entries per
+// row and tile).  lmap keeps each slot's original l; pull_reduce_kernel writes the sums back
+// in CBSR order.  Slot of sorted position p: lane q = p % (k/4), instruction i = p / (k/4)
+// -> slot 4q + i.  Equal selectors (never produced by top-k) rank by l, so the map is a
+// permutation of the k slots whatever the input.
+__global__ __launch_bounds__(kBlock) void pull_sel_kernel(const uint8_t *__restrict__ sel,
+                                                          uint8_t *__restrict__ sel_q,
+                                                          uint8_t *__restrict__ lmap,
+                                                          int64_t num_cols, int k, int kp) {
+    __shared__ uint32_t bm[kBlock / 4 * 8];  // 256-bit column set per destination
+    __shared__ uint8_t s_out[kBlock], l_out[kBlock];
+    const int nd = kBlock / k;  // destinations per block (k % 4 == 0, k <= 256)
+    const int tid = threadIdx.x;
+    const int d = tid / k, l = tid % k;
+    const int64_t c0 = (int64_t)blockIdx.x * nd;
+    const int64_t c = c0 + d;
+    const bool act = d < nd && c < num_cols;
+    for (int i = tid; i < nd * 8; i += kBlock) bm[i] = 0u;
+    __syncthreads();
+    const uint32_t s = act ? sel[c * k + l] : 0u;
+    if (act) atomicOr(&bm[d * 8 + (s >> 5)], 1u << (s & 31));
+    __syncthreads();
+    if (act) {
+        int distinct = 0, rank = 0;
+        for (int wd = 0; wd < 8; ++wd) {
+            const uint32_t b = bm[d * 8 + wd];
+            distinct += __popc(b);
+            if (wd < (int)(s >> 5)) rank += __popc(b);
+        }
+        rank += __popc(bm[d * 8 + (s >> 5)] & ((1u << (s & 31)) - 1u));
+        if (distinct < k) {  // repeated selectors: rank by (selector, l)
+            rank = 0;
+            for (int m = 0; m < k; ++m) {
+                const uint32_t sm = sel[c * k + m];
+                rank += (sm < s) || (sm == s && m < l);
+            }
+        }
+        // part h = rank / kp (pull_q_kernel's parts), then the quantile slot inside it
+        const int q4 = kp / 4, h = rank / kp, r = rank % kp;
+        const int slot = h * kp + 4 * (r % q4) + r / q4;
+        s_out[d * k + slot] = (uint8_t)s;
+        l_out[d * k + slot] = (uint8_t)l;
+    }
+    __syncthreads();
+    const int64_t nb = (num_cols - c0 < nd ? num_cols - c0 : nd) * (int64_t)k;
+    if (tid < nb) {
+        sel_q[c0 * k + tid] = s_out[tid];
+        lmap[c0 * k + tid] = l_out[tid];
+    }
+}
+
+// Parts: with H = k / kp parts, destination c's slots split by sorted position into H
+// groups of kp (part h: the h-th kp smallest selectors), and one workgroup sums one part of
+// one tile: the accumulator holds kp slots per destination, so a bucket holds H times the
+// destinations and a source row meets ~H times fewer buckets; each part's gathers cover
+// only its share of a row's columns (the h-th kp order statistics of every entry).  The
+// tile's entries are read H times.  Model of the Reddit stream (k = 16): L2 lines per entry
+// 3.2 -> 2.3 at H = 2.
+// One 1024-thread workgroup per (tile, part), as pull_tile_kernel (fp64 LDS accumulator of
+// the bucket, its slot-ordered selector rows copied next to it), with:
+//  * quantile slots (above): lane q's u32 selector word holds its four instructions'
+//    columns;
+//  * a two-step software pipeline: step n's gathers are issued before step n-1's adds, and
+//    the entries two steps ahead, so a wave keeps 2 x 4U gathers in flight and never waits
+//    on loads it has just issued (the one-step loop waited for every load at its head);
+//  * the G' gathers through a wave-uniform buffer descriptor over the slice's rows with
+//    32-bit offsets (no 64-bit address math per value); a selector >= D (possible only
+//    when D < 256, !FULLD) gets an offset past the descriptor, and the hardware returns 0;
+//  * tiles in XCD order (MAXK_PULL_XCD): XCD x runs the x-th eighth of the tile sequence
+//    in order, so each XCD's L2 holds the one slice it works on instead of every XCD
+//    pulling every slice.
+template <int LR, int U, bool FULLD>
+__global__ __launch_bounds__(1024) void pull_q_kernel(
+    const float *__restrict__ Gp, const uint8_t *__restrict__ sel_q,
+    const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
+    float *__restrict__ tile_out, int64_t num_cols, int n_buckets, int n_tiles,
+    int rows_per_slice, int64_t num_rows, int D, int k, int kp, int shift) {
+    extern __shared__ double acc[];  // [(kp + 1) << shift], then [kp << shift] selector bytes
+    constexpr int EPI = kWave / LR;                 // entries per wave instruction
+    constexpr int STEP = EPI * U;                   // entries per wave step
+    constexpr int NL = (STEP + kWave - 1) / kWave;  // entry loads per step (one per lane)
+    const int tid = threadIdx.x;
+    const int lane = lane_id(), w = tid / kWave;
+    const int g = lane / LR, q = lane % LR;
+    const bool qok = q < kp / 4;
+    const int ks = kp + 1;
+    const int H = k / kp;
+    const int tp = MAXK_PULL_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    if (tp >= n_tiles * H) return;  // the XCD grid's padding
+    const int t = tp / H, h = tp % H;
+    const int j = t % n_buckets;
+    const int64_t r0 = (int64_t)(t / n_buckets) * rows_per_slice;
+    const int64_t nrows = num_rows - r0 < rows_per_slice ? num_rows - r0 : rows_per_slice;
+    const float *__restrict__ Gs = Gp + r0 * D;
+    const int s0 = tile_ptr[t], s1 = tile_ptr[t + 1];
+    const int64_t c0 = (int64_t)j << shift;
+    uint8_t *sel_lds = reinterpret_cast<uint8_t *>(acc + (ks << shift));
+    for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
+    {  // part h of each destination's slot-ordered selectors: kp bytes of its k-byte row
+        const uint8_t *__restrict__ selg = sel_q + c0 * k + h * kp;
+        const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
+        if (kp == k) {
+            const int nb = rows * k;  // c0 * k is a multiple of 16 (shift >= 4), as is sel_lds
+            for (int i = tid; i < nb / 16; i += 1024)
+                reinterpret_cast<uint4 *>(sel_lds)[i] = reinterpret_cast<const uint4 *>(selg)[i];
+            for (int i = (nb & ~15) + tid; i < nb; i += 1024) sel_lds[i] = selg[i];
+        } else {  // kp % 4 == 0: 4-byte words
+            const int wpr = kp / 4;
+            for (int i = tid; i < rows * wpr; i += 1024)
+                reinterpret_cast<uint32_t *>(sel_lds)[i] =
+                    *reinterpret_cast<const uint32_t *>(selg + (i / wpr) * k + (i % wpr) * 4);
+        }
+    }
+    __syncthreads();
+    const auto grs = wave_buffer(Gs, (uint32_t)(nrows > 0 ? nrows : 0) * (uint32_t)D * 4u);
+    const auto ers = wave_buffer(ent + s0, (uint32_t)(s1 - s0) * 8u);
+    const uint32_t Db = (uint32_t)D * 4u;
+    const int stride = 16 * STEP;  // 16 waves
+    const int base = w * STEP;     // entry offsets relative to s0
+    const int n_e = s1 - s0;
+    // Every step is issued the same way: no load sits under a branch, since the compiler
+    // merges the counters of the two sides of a branch conservatively and then waits for
+    // loads it could leave in flight.  Entries past the tile read 0 (past the descriptor),
+    // their gathers get offsets past the G' descriptor (0, no memory access), their weight
+    // 0, and their adds (+0.0) go to a lane-private row of the accumulator.  The loop runs
+    // an even number of steps; the last issue is never consumed.
+    const int nsteps = base < n_e ? (n_e - base + stride - 1) / stride : 0;
+    const int idle = (w * kWave + lane) & ((1 << shift) - 1);
+
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 myA[NL], myB[NL];
+    float vA[U][4], vB[U][4];
+    int dA[U], dB[U];
+    float wA[U], wB[U];
+    auto load_ent = [&](u32x2(&my)[NL], int n) {
+#pragma unroll
+        for (int m = 0; m < NL; ++m)
+            my[m] = __builtin_amdgcn_raw_buffer_load_b64(
+                ers, (int)((uint32_t)(base + n * stride + m * kWave + lane) * 8u), 0, 0);
+    };
+    // step n: entries from my (then reloaded for step n + 2), selectors, gathers into v
+    auto issue = [&](u32x2(&my)[NL], float(&v)[U][4], int(&dc)[U], float(&wc)[U], int n) {
+        uint32_t ex[U], ey[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int m = (u * EPI) / kWave;  // compile-time after unrolling
+            const int src = (u * EPI + g - m * kWave) * 4;
+            ex[u] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)my[m][0]);
+            ey[u] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)my[m][1]);
+        }
+        load_ent(my, n + 2);
+        uint32_t sv[U];
+        bool ok[U];
+        const int eb = base + n * stride + g;  // this lane group's entry of instruction 0
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            ok[u] = eb + u * EPI < n_e && qok;
+            const int d = ok[u] ? (int)(ex[u] >> 16) : idle;
+            dc[u] = d * ks + 4 * q * ok[u];
+            sv[u] = *reinterpret_cast<const uint32_t *>(sel_lds + d * kp + (ok[u] ? q * 4 : 0));
+            wc[u] = ok[u] ? __uint_as_float(ey[u]) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ro = ok[u] ? (ex[u] & 0xffffu) * Db : 0x80000000u;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t c = (sv[u] >> (8 * i)) & 255u;
+                uint32_t off = ro + c * 4u;
+                if (!FULLD) off = c < (uint32_t)D ? off : 0x80000000u;  // past the buffer: 0
+                v[u][i] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(grs, (int)off, 0, 0));
+            }
+        }
+    };
+    auto consume = [&](float(&v)[U][4], int(&dc)[U], float(&wc)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            double *a = &acc[dc[u]];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) atomicAdd(a + i, (double)(wc[u] * v[u][i]));
+        }
+    };
+    if (nsteps > 0) {
+        load_ent(myA, 0);
+        load_ent(myB, 1);
+        // keep step 1's entries ahead of step 0's gathers: the loop head waits for them with
+        // step 0's gathers still in flight only if they were issued first
+        __builtin_amdgcn_sched_barrier(0);
+        issue(myA, vA, dA, wA, 0);
+        // sched_barrier: the machine scheduler would otherwise hoist a consume's multiplies
+        // and the next issue's shuffles above the gathers, waiting for loads meant to stay in
+        // flight
+        for (int n = 0; n < nsteps; n += 2) {
+            issue(myB, vB, dB, wB, n + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(vA, dA, wA);
+            __builtin_amdgcn_sched_barrier(0);
+            issue(myA, vA, dA, wA, n + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            consume(vB, dB, wB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    __syncthreads();
+    // tile_out[t] is [2^shift, k] in slot order; part h fills slots [h * kp, (h + 1) * kp)
+    float *o = tile_out + (size_t)t * ((size_t)k << shift) + h * kp;
+    const int w4 = kp / 4;
+    for (int i4 = tid; i4 < (kp << shift) / 4; i4 += 1024) {
+        const int c = i4 / w4, s4 = i4 % w4;
+        const double *a = &acc[c * ks + 4 * s4];
+        *reinterpret_cast<float4 *>(o + (size_t)c * k + 4 * s4) =
+            make_float4((float)a[0], (float)a[1], (float)a[2], (float)a[3]);
+    }
+}
+
+// grad_cbsr rows of bucket j = the sum of its slices' tiles, in slice order.  With lmap
+// (pull_q_kernel's slot order, k % 4 == 0) slot f of row c goes to l = lmap[c * k + f].
 __global__ __launch_bounds__(kBlock) void pull_reduce_kernel(const float *__restrict__ tile_out,
+                                                             const uint8_t *__restrict__ lmap,
                                                              float *__restrict__ grad_cbsr,
                                                              int64_t num_cols, int n_buckets,
                                                              int slices, int k, int shift) {
@@ -714,6 +948,16 @@ __global__ __launch_bounds__(kBlock) void pull_reduce_kernel(const float *__rest
         a.y += b.y;
         a.z += b.z;
         a.w += b.w;
+    }
+    if (lmap) {  // four slots of one row (k % 4 == 0) back to their l
+        const size_t f0 = (size_t)c0 * k + (size_t)i * 4;
+        const uint32_t m = *reinterpret_cast<const uint32_t *>(lmap + f0);
+        float *row = grad_cbsr + (f0 / k) * k;
+        row[m & 255u] = a.x;
+        row[(m >> 8) & 255u] = a.y;
+        row[(m >> 16) & 255u] = a.z;
+        row[m >> 24] = a.w;
+        return;
     }
     reinterpret_cast<float4 *>(grad_cbsr + c0 * k)[i] = a;
 }
@@ -1051,14 +1295,32 @@ extern "C" int maxk_sspmm_backward_bucket(const int32_t *row_ptr, const int32_t 
 }
 
 // ---- pull backward: C entry ------------------------------------------------------------
+namespace maxk {
+// Parts of pull_q_kernel for k and a plan's bucket shift: the fewest H (k % (4H) == 0) whose
+// accumulator [(k/H + 1) << shift] doubles and selector rows [k/H << shift] bytes fit the
+// LDS; 0 if none does.
+int pull_parts(int k, int shift) {
+    for (int H = 1; H <= k / 4; H *= 2) {
+        if (k % (4 * H)) break;
+        const int kp = k / H;
+        if ((((size_t)(kp + 1) * 8 + kp) << shift) <= kPullLdsBytes) return H;
+    }
+    return 0;
+}
+}  // namespace maxk
+
 extern "C" size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int64_t num_cols,
                                                           int32_t dim_origin, int32_t dim_k,
                                                           int32_t slices) {
     if (num_rows < 0 || num_cols < 0 || dim_origin <= 0 || dim_k <= 0 || slices <= 0) return 0;
-    const int shift = maxk_bucket_shift(dim_k);  // the largest shift: bounds every plan's
+    // the largest shift any plan may carry bounds the tile partials
+    const int shift = std::max(maxk_bucket_shift(dim_k), maxk_pull_shift(dim_k));
     const int64_t nb = maxk_bucket_count(num_cols, shift);
     const size_t gp = ((size_t)num_rows * dim_origin * sizeof(float) + 255) & ~(size_t)255;
-    return gp + (size_t)slices * nb * ((size_t)dim_k << shift) * sizeof(float);
+    const size_t tiles = (size_t)slices * nb * ((size_t)dim_k << shift) * sizeof(float);
+    // slot-ordered selectors and their l map (pull_sel_kernel), k % 4 == 0
+    const size_t selq = dim_k % 4 == 0 ? 2 * (((size_t)num_cols * dim_k + 255) & ~(size_t)255) : 0;
+    return gp + tiles + selq;
 }
 
 extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
@@ -1074,10 +1336,16 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
                  "pull backward needs dim_k %% 4 == 0 or dim_k <= 64, got %d", dim_k);
     MAXK_REQUIRE(dim_origin % 4 == 0, "pull backward needs dim_origin %% 4 == 0, got %d",
                  dim_origin);
-    MAXK_REQUIRE(bucket_shift >= 4 && bucket_shift <= maxk_bucket_shift(dim_k) &&
-                     bucket_shift <= 15,
-                 "bucket_shift %d out of range [4, min(15, maxk_bucket_shift(%d) = %d)]",
-                 bucket_shift, dim_k, maxk_bucket_shift(dim_k));
+    const bool v4 = dim_k % 4 == 0;
+    // quantile-slot form with H parts (k % 4 == 0), else the one-l-per-lane pull_tile_kernel
+    const int parts = MAXK_PULL_Q && v4 && bucket_shift >= 4 && bucket_shift <= 15
+                          ? pull_parts(dim_k, bucket_shift)
+                          : 0;
+    const int max_shift = std::max(maxk_bucket_shift(dim_k), maxk_pull_shift(dim_k));
+    MAXK_REQUIRE(bucket_shift >= 4 && bucket_shift <= 15 && bucket_shift <= max_shift &&
+                     (parts > 0 || bucket_shift <= maxk_bucket_shift(dim_k)),
+                 "bucket_shift %d out of range [4, min(15, %d)] for dim_k %d", bucket_shift,
+                 max_shift, dim_k);
     const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
     MAXK_REQUIRE(slices >= 1 && slices * nb < (1LL << 31), "slices %d out of range", slices);
     const int64_t rps = (num_rows + slices - 1) / slices;
@@ -1111,8 +1379,43 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     const size_t lds = acc_b + (sel_lds ? sel_b : 0);
     const uint2 *ent2 = reinterpret_cast<const uint2 *>(ent);
     // four l per lane (one u32 selector read) when k % 4 == 0, else one
-    const bool v4 = k % 4 == 0;
-    switch (lanes_per_edge(v4 ? k / 4 : k) * 4 + (sel_lds ? 1 : 0) + (v4 ? 2 : 0)) {
+    const uint8_t *lmap = nullptr;
+    if (parts > 0) {  // quantile-slot form (pull_q_kernel), `parts` workgroups per tile
+        const int kp = k / parts;
+        const size_t lds_q = ((size_t)(kp + 1) * 8 + kp) << bucket_shift;
+        const size_t tb = (size_t)slices * nb * ((size_t)k << bucket_shift) * sizeof(float);
+        const size_t nsel = ((size_t)num_cols * k + 255) & ~(size_t)255;
+        uint8_t *sel_q = reinterpret_cast<uint8_t *>(tile_out) + tb;
+        uint8_t *lm = sel_q + nsel;
+        const int nd = kBlock / k;
+        hipLaunchKernelGGL(pull_sel_kernel, dim3((unsigned)ceil_div(num_cols, nd)), dim3(kBlock),
+                           0, s, cbsr_idx, sel_q, lm, num_cols, k, kp);
+        MAXK_LAUNCHED("pull_sel_kernel");
+        const int64_t work = (int64_t)tiles * parts;
+        const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);
+        const bool fulld = dim_origin == kMaxDim;
+        switch (lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
+#define MAXK_CASE(LRV)                                                                        \
+    case LRV * 2 + 1:                                                                         \
+        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_U, true>), dim3(grid), dim3(1024),    \
+                           lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
+                           (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
+        break;                                                                                \
+    case LRV * 2:                                                                             \
+        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_U, false>), dim3(grid), dim3(1024),   \
+                           lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
+                           (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
+        break;
+            MAXK_CASE(1) MAXK_CASE(2) MAXK_CASE(4) MAXK_CASE(8) MAXK_CASE(16) MAXK_CASE(32)
+            MAXK_CASE(64)
+#undef MAXK_CASE
+            default:
+                set_error("unsupported lane group");
+                return MAXK_ERR_INVALID;
+        }
+        MAXK_LAUNCHED("pull_q_kernel");
+        lmap = lm;
+    } else switch (lanes_per_edge(v4 ? k / 4 : k) * 4 + (sel_lds ? 1 : 0) + (v4 ? 2 : 0)) {
 #define MAXK_CASE(LRV, SL)                                                                    \
     case LRV * 4 + SL + 2:                                                                    \
         hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL, 4>), dim3(tiles), dim3(1024), \
@@ -1139,8 +1442,8 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     MAXK_LAUNCHED("pull_tile_kernel");
     hipLaunchKernelGGL(pull_reduce_kernel,
                        dim3((unsigned)nb, (unsigned)ceil_div(ceil_div((int64_t)k << bucket_shift, 4), kBlock)),
-                       dim3(kBlock), 0, s, tile_out, grad_cbsr, num_cols, (int)nb, slices, k,
-                       bucket_shift);
+                       dim3(kBlock), 0, s, tile_out, lmap, grad_cbsr, num_cols, (int)nb, slices,
+                       k, bucket_shift);
     MAXK_LAUNCHED("pull_reduce_kernel");
     return MAXK_OK;
 }

@@ -5,6 +5,8 @@
 // the CSC side files of generate_meta_csc.py:14-93 / load_warp4_metadata_csc.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace maxk {
@@ -235,9 +237,21 @@ size_t pull_sort_temp_bytes(int64_t num_e, int64_t n_tiles) {
 }  // namespace
 }  // namespace maxk
 
+// The widest bucket that up to MAXK_PULL_H parts reach (pull_q_kernel, k % (4H) == 0) while
+// a part keeps at least MAXK_PULL_MIN_KP slots: the accumulator holds k/H slots per
+// destination.  Reddit: k = 32 / 64 at H = 2 took 3.93 / 6.28 ms against 4.20 / 8.13 at H = 1;
+// k = 16 at H = 2 (8 slots) 2.72 against 2.62 (profiles/r02/tune/pull_parts.txt).  A part
+// count that does not widen the bucket is not used.  At least 4: the backward copies a
+// bucket's selector rows 16 B at a time (16 | 2^shift * k).
 extern "C" int maxk_pull_shift(int32_t dim_k) {
-    const int s = maxk_bucket_shift(dim_k);
-    return s < 0 ? s : (s > MAXK_PULL_SHIFT_DELTA ? s - MAXK_PULL_SHIFT_DELTA : 0);
+    if (dim_k <= 0) return -1;
+    int s = maxk_bucket_shift(dim_k);
+    for (int H = 2; MAXK_PULL_Q && H <= MAXK_PULL_H && dim_k % (4 * H) == 0 &&
+                    dim_k / H >= MAXK_PULL_MIN_KP;
+         H *= 2)
+        s = std::max(s, maxk_bucket_shift(dim_k / H));
+    const int p = s - MAXK_PULL_SHIFT_DELTA;
+    return p < 4 ? 4 : (p > 15 ? 15 : p);
 }
 
 // ~3.5 MiB of G rows per slice up to k = 16, k/16 times that above: the S tile partials
@@ -269,7 +283,7 @@ extern "C" int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx,
     MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
     MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
     MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
-    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 15, "bucket_shift must be in [0,15]");
+    MAXK_REQUIRE(bucket_shift >= 4 && bucket_shift <= 15, "bucket_shift must be in [4,15]");
     const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
     MAXK_REQUIRE(slices >= 1 && slices * nb < (1LL << 31), "slices %d out of range", slices);
     const int64_t rps64 = (num_rows + slices - 1) / slices;

@@ -74,8 +74,11 @@ _CHECKED: "dict" = {}
 
 def _check_graph_once(row_ptr, col_idx, num_cols):
     """Out-of-range row_ptr / col_idx are the only inputs that can make a kernel read out of
-    bounds (a u8 selector always indexes inside a 256-entry row), so each graph is validated
-    the first time it is used; the check is cached on the tensors' identity and versions."""
+    bounds, so each graph is validated the first time it is used; the check is cached on the
+    tensors' identity and versions.  Selectors change every call and are not checked here:
+    a selector >= D contributes nothing in every kernel (the forward sends it to a trash
+    column, the two-phase and atomic backwards read a zeroed LDS slot, the pull backward
+    gathers 0 for it), so it cannot read outside G or another row of it."""
     key = (id(row_ptr), id(col_idx))
     hit = _CHECKED.get(key)
     if hit is not None:
@@ -317,8 +320,9 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     buckets of 2^shift; per tile
     (slice, bucket) the edges in CSR order, each {row in its slice | column in its bucket
     << 16, weight bits}.  Built on the GPU (one stable radix sort); cached per
-    (indices, values) tensor objects and their version counters -- the weights are copied
-    into the plan, so a plan serves the values it was built from."""
+    (indptr, indices, values) tensor objects and their version counters -- indptr assigns
+    the edges to rows and slices, and the weights are copied into the plan, so a plan serves
+    the graph and values it was built from."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32)):
         _need(t, n, dt)
@@ -328,11 +332,12 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
         raise RuntimeError(f"pull_plan: invalid k {k}")
     num_rows = indptr.numel() - 1
     S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(dim), int(k)))
-    key = (id(indices), id(values), shift, S)
+    key = (id(indptr), id(indices), id(values), shift, S)
     hit = _PULL_CACHE.get(key)
     if cache and hit is not None:
-        ri, rv, nc, vi, vv, plan = hit
-        if (ri() is indices and rv() is values and nc == num_cols and vi == indices._version
+        rp, ri, rv, nc, pv, vi, vv, plan = hit
+        if (rp() is indptr and ri() is indices and rv() is values and nc == num_cols
+                and pv == indptr._version and vi == indices._version
                 and vv == values._version):
             return plan
     dev = indices.device
@@ -349,10 +354,11 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     plan = (tptr, ent, shift, S)
     if cache:
         if key not in _PULL_CACHE:
-            weakref.finalize(indices, _PULL_CACHE.pop, key, None)
-            weakref.finalize(values, _PULL_CACHE.pop, key, None)
-        _PULL_CACHE[key] = (weakref.ref(indices), weakref.ref(values), int(num_cols),
-                            indices._version, values._version, plan)
+            for t in (indptr, indices, values):
+                weakref.finalize(t, _PULL_CACHE.pop, key, None)
+        _PULL_CACHE[key] = (weakref.ref(indptr), weakref.ref(indices), weakref.ref(values),
+                            int(num_cols), indptr._version, indices._version, values._version,
+                            plan)
     return plan
 
 
@@ -421,8 +427,9 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     mode "auto" (default; MAXK_BWD_MODE overrides): "pull" or "csc", see _bwd_mode.
     mode "pull": per tile (row slice, destination bucket), the k values of every edge
     gathered from G / row_div and summed in fp64 LDS accumulators, no contribution rows;
-    uses the graph's pull plan (built once per (indices, values) and cached, or `plan=`
-    from pull_plan()); deterministic.
+    uses the graph's pull plan (built once per (indptr, indices, values) and cached, or
+    `plan=` from pull_plan()); fp64 tile sums, so two runs agree except in rare rounding
+    ties (use "csc" for bitwise repeatability).
     mode "bucket": two-phase with a bucketed phase 2 summing in fp64 LDS accumulators, using
     the graph's bucket plan (built once and cached, or `plan=` from bucket_plan()).
     mode "csc": two-phase, atomic-free and bitwise deterministic, using the graph's

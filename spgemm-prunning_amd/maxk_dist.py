@@ -7,15 +7,22 @@ those vertices.  There is no reference counterpart (the reference is
 single-GPU); the oracle for this path is "identical to the
 1-GPU result".
 
-Per aggregation:
-  forward   all-gather of the CBSR rows (k f32 + k u8 per vertex; the only
-            exchange), then the local row-wise SpGEMM over the owned rows;
-  backward  local push of the owned rows' contributions into a CBSR-shaped
-            gradient for ALL vertices, then a reduce-scatter that sums the
-            partials on the owners (k f32 per vertex).
-Vertex ids are remapped once to a padded space (owner * vmax + local row), so
-both collectives are plain equal-size all_gather_into_tensor /
-reduce_scatter_tensor calls.
+Two exchange modes, the same result:
+  "gather" (default)  forward: one all-gather of every vertex's CBSR row (k f32 +
+            k u8); backward: the local push into a CBSR-shaped gradient for ALL
+            vertices, then a reduce-scatter that sums the partials on the owners.
+            Vertex ids are remapped once to a padded space (owner * vmax + local
+            row), so both collectives are plain equal-size calls.
+  "halo"    only the rows a shard's edges touch travel: once per graph each rank
+            sends every owner the sorted list of the owner's vertices it needs
+            (all-to-allv), which becomes the owner's send plan.  Forward: one
+            all-to-allv of the needed CBSR rows into a compact column space (the
+            shard's halo, in global-id order); backward: the local push into that
+            compact space, one all-to-allv back to the owners, and each owner adds
+            what it receives into its rows (index_add).  Bytes per step and rank:
+            halo rows x k x 5 each way instead of (world-1)/world x V x k x 5
+            (exchange_bytes()).  On graphs without locality (the randomly
+            labelled synthetic ones) a shard's halo is nearly every vertex.
 
 `kernels` is the compute backend: by default the HIP library through
 maxk_cuda_kernels; the CPU tests inject an object with the same two methods
@@ -56,6 +63,16 @@ def reduce_scatter_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> Non
         dist.reduce_scatter_tensor(out, inp, group=group)
 
 
+def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None):
+    """all_to_all_single along dim 0 (None splits: equal); gloo is staged through host."""
+    if _staged(group) and inp.is_cuda:
+        tmp = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(tmp, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(tmp)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
 def balanced_bounds(row_ptr: torch.Tensor, world: int) -> List[int]:
     """Row boundaries [0 = b0 <= b1 <= ... <= b_world = V] with ~E/world edges per shard."""
     rp = row_ptr.detach().to("cpu", torch.int64)
@@ -88,12 +105,20 @@ class _HipKernels:
 
 
 class ShardedMaxK:
-    """Rank-local view of a vertex-partitioned graph for the MaxK aggregation."""
+    """Rank-local view of a vertex-partitioned graph for the MaxK aggregation.
+
+    mode "gather": column space = padded [world * vmax] (all vertices);
+    mode "halo":   column space = this shard's halo (the distinct columns of its edges, in
+                   global-id order).  n_cols is its size either way."""
+
+    MODES = ("gather", "halo")
 
     def __init__(self, row_ptr: torch.Tensor, col_idx: torch.Tensor, values: torch.Tensor,
                  rank: int, world: int, group=None, device=None, kernels=None,
-                 bounds: Optional[List[int]] = None):
-        self.rank, self.world, self.group = rank, world, group
+                 bounds: Optional[List[int]] = None, mode: str = "gather"):
+        if mode not in self.MODES:
+            raise ValueError(f"mode must be one of {self.MODES}, got {mode!r}")
+        self.rank, self.world, self.group, self.mode = rank, world, group, mode
         self.device = torch.device(device) if device is not None else row_ptr.device
         self.kernels = kernels if kernels is not None else _HipKernels()
         self.bounds = bounds if bounds is not None else balanced_bounds(row_ptr, world)
@@ -102,37 +127,88 @@ class ShardedMaxK:
         self.v0, self.v1 = b[rank], b[rank + 1]
         self.n_local = self.v1 - self.v0
         self.vmax = max(max(b[i + 1] - b[i] for i in range(world)), 1)
-        self.n_cols = world * self.vmax
         rp = row_ptr.to(self.device, torch.int64)
         e0, e1 = int(rp[self.v0]), int(rp[self.v1])
         self.row_ptr = (rp[self.v0:self.v1 + 1] - e0).to(torch.int32).contiguous()
         cols = col_idx[e0:e1].to(self.device, torch.int64)
         starts = torch.tensor(b, dtype=torch.int64, device=self.device)
-        owner = torch.searchsorted(starts[1:], cols, right=True)
-        self.col_idx = (owner * self.vmax + (cols - starts[owner])).to(torch.int32).contiguous()
+        if mode == "gather":
+            owner = torch.searchsorted(starts[1:], cols, right=True)
+            self.col_idx = (owner * self.vmax + (cols - starts[owner])).to(torch.int32).contiguous()
+            self.n_cols = world * self.vmax
+        else:
+            self._halo_plan(cols, starts)
         self.values = values[e0:e1].to(self.device, torch.float32).contiguous()
         self._plans = {}
 
+    # ---- halo send plan (once per graph)
+    def _halo_plan(self, cols: torch.Tensor, starts: torch.Tensor) -> None:
+        halo = torch.unique(cols)  # sorted global ids: grouped by owner, owners ascending
+        self.halo = halo
+        self.n_cols = int(halo.numel())
+        self.col_idx = torch.searchsorted(halo, cols).to(torch.int32).contiguous()
+        owner = torch.searchsorted(starts[1:], halo, right=True)
+        need = torch.bincount(owner, minlength=self.world)  # rows I receive from each owner
+        give = torch.empty_like(need)                       # rows each requester wants of mine
+        _all_to_all(give, need, None, None, self.group)
+        self.recv_counts = [int(x) for x in need.tolist()]
+        self.send_counts = [int(x) for x in give.tolist()]
+        req = torch.empty(sum(self.send_counts), dtype=torch.int64, device=self.device)
+        _all_to_all(req, halo, self.send_counts, self.recv_counts, self.group)
+        self.send_rows = (req - self.v0).contiguous()  # my local rows, per requester in order
+
+    def exchange_bytes(self, k: int) -> dict:
+        """Bytes this rank sends / receives per step (forward CBSR + backward gradient)."""
+        row_f, row_b = k * 5, k * 4  # k f32 + k u8 forward, k f32 backward
+        if self.mode == "gather":
+            others = self.n_cols - self.vmax
+            return {"fwd_recv": others * row_f, "fwd_send": (self.world - 1) * self.vmax * row_f,
+                    "bwd_send": others * row_b, "bwd_recv": (self.world - 1) * self.vmax * row_b}
+        own = self.recv_counts[self.rank]
+        recv_rows = self.n_cols - own
+        send_rows = sum(self.send_counts) - self.send_counts[self.rank]
+        return {"fwd_recv": recv_rows * row_f, "fwd_send": send_rows * row_f,
+                "bwd_send": recv_rows * row_b, "bwd_recv": send_rows * row_b}
+
     # ---- helpers
     def gather_cbsr(self, val_local: torch.Tensor, idx_local: torch.Tensor):
-        """All-gather the CBSR rows of every shard into the padded [world*vmax, k] space.
+        """The CBSR rows of the shard's column space: [n_cols, k] values and selectors.
 
-        One collective: each rank sends one byte chunk [vmax*k values | vmax*k selectors]
-        (padding rows zero), so the values and selectors travel in a single all-gather
-        instead of two; the two halves are then split out of the gathered chunks."""
+        One collective per call: each row travels as one byte record [k values | k selectors],
+        so values and selectors move together; "gather" all-gathers every rank's vmax rows
+        (padding rows zero), "halo" sends each owner's requested rows only."""
         k = val_local.shape[1]
         dev = val_local.device
-        nv = self.vmax * k
-        vb = nv * val_local.element_size()
-        chunk = vb + nv * idx_local.element_size()
-        send = torch.zeros(chunk, dtype=torch.uint8, device=dev)
-        send[:vb].view(val_local.dtype).view(self.vmax, k)[:self.n_local] = val_local
-        send[vb:].view(idx_local.dtype).view(self.vmax, k)[:self.n_local] = idx_local
-        recv = torch.empty(self.world, chunk, dtype=torch.uint8, device=dev)
-        all_gather_rows(recv.view(-1), send, self.group)
+        vb = k * val_local.element_size()
+        rb = vb + k * idx_local.element_size()
+        if self.mode == "gather":
+            send = torch.zeros(self.vmax, rb, dtype=torch.uint8, device=dev)
+            send[:self.n_local, :vb] = val_local.contiguous().view(torch.uint8).view(-1, vb)
+            send[:self.n_local, vb:] = idx_local.contiguous().view(torch.uint8).view(-1, rb - vb)
+            recv = torch.empty(self.world * self.vmax, rb, dtype=torch.uint8, device=dev)
+            all_gather_rows(recv.view(-1), send.view(-1), self.group)
+        else:
+            rows = self.send_rows.to(dev)
+            send = torch.empty(rows.numel(), rb, dtype=torch.uint8, device=dev)
+            send[:, :vb] = val_local.contiguous().view(torch.uint8).view(-1, vb)[rows]
+            send[:, vb:] = idx_local.contiguous().view(torch.uint8).view(-1, rb - vb)[rows]
+            recv = torch.empty(self.n_cols, rb, dtype=torch.uint8, device=dev)
+            _all_to_all(recv, send, self.recv_counts, self.send_counts, self.group)
         val_all = recv[:, :vb].contiguous().view(val_local.dtype).view(self.n_cols, k)
         idx_all = recv[:, vb:].contiguous().view(idx_local.dtype).view(self.n_cols, k)
         return val_all, idx_all
+
+    def scatter_grad(self, partial: torch.Tensor) -> torch.Tensor:
+        """Sum the per-rank partial gradients [n_cols, k] onto the owners: [n_local, k]."""
+        k = partial.shape[1]
+        if self.mode == "gather":
+            out = torch.empty(self.vmax, k, dtype=partial.dtype, device=partial.device)
+            reduce_scatter_rows(out, partial.contiguous(), self.group)
+            return out[:self.n_local]
+        recv = torch.empty(sum(self.send_counts), k, dtype=partial.dtype, device=partial.device)
+        _all_to_all(recv, partial.contiguous(), self.send_counts, self.recv_counts, self.group)
+        out = torch.zeros(self.n_local, k, dtype=partial.dtype, device=partial.device)
+        return out.index_add_(0, self.send_rows.to(partial.device), recv)
 
     def plan(self, k: int, D: Optional[int] = None):
         """The backward's per-graph plan at width k and feature width D (built once per
@@ -152,15 +228,13 @@ class ShardedMaxK:
 
     def backward(self, grad_local: torch.Tensor, idx_all: torch.Tensor,
                  row_div_local=None) -> torch.Tensor:
-        """CBSR gradient of the owned vertices [n_local, k] (partials summed by reduce-scatter)."""
+        """CBSR gradient of the owned vertices [n_local, k] (partials summed on the owners)."""
         partial = self.kernels.sspmm_backward(self.row_ptr, self.col_idx, self.values,
                                               grad_local.contiguous(), idx_all,
                                               row_div=row_div_local,
                                               plan=self.plan(idx_all.shape[1],
                                                              grad_local.shape[1]))
-        out = torch.empty(self.vmax, partial.shape[1], dtype=partial.dtype, device=partial.device)
-        reduce_scatter_rows(out, partial.contiguous(), self.group)
-        return out[:self.n_local]
+        return self.scatter_grad(partial)
 
 
 class ShardedMaxKFunction(Function):

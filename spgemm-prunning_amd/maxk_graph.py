@@ -144,9 +144,20 @@ PRESETS = {
 }
 
 
-def make_graph(V, E, alpha, i0, seed, device):
+def make_graph(V, E, alpha, i0, seed, device, trace=None):
     """Symmetric Chung-Lu power-law graph with self loops, deduplicated, CSR with sorted
-    columns (the shape dataset_gen.py:44-115 produces), exactly E edges when E-V is even."""
+    columns (the shape dataset_gen.py:44-115 produces), exactly E edges when E-V is even.
+    `trace` (a list) collects (stage, seconds) pairs, each stage synchronised."""
+    import time
+    t_last = [time.perf_counter()]
+
+    def mark(name):
+        if trace is not None:
+            if torch.device(device).type == "cuda":
+                torch.cuda.synchronize(device)
+            t = time.perf_counter()
+            trace.append((name, round(t - t_last[0], 3)))
+            t_last[0] = t
     g = torch.Generator(device=device).manual_seed(seed)
     pairs_target = (E - V) // 2
     w = (torch.arange(V, device=device, dtype=torch.float64) + i0) ** (-alpha)
@@ -162,8 +173,10 @@ def make_graph(V, E, alpha, i0, seed, device):
         b.clamp_(max=V - 1)
         lo, hi = torch.minimum(a, b), torch.maximum(a, b)
         k = (lo * V + hi)[lo != hi]
+        mark("sample")
         keys = torch.unique(torch.cat([keys, k]))
         need = pairs_target - keys.numel()
+        mark("unique")
         del a, b, lo, hi, k
     keys = keys[torch.randperm(keys.numel(), generator=g, device=device)[:pairs_target]]
     relabel = torch.randperm(V, generator=g, device=device)
@@ -173,8 +186,10 @@ def make_graph(V, E, alpha, i0, seed, device):
     src = torch.cat([lo, hi, loops])
     dst = torch.cat([hi, lo, loops])
     del lo, hi
+    mark("permute")
     key = torch.sort(src * V + dst).values
     del src, dst
+    mark("sort")
     src, dst = key // V, key % V
     row_ptr = torch.zeros(V + 1, dtype=torch.int64, device=device)
     row_ptr[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)

@@ -43,6 +43,29 @@ def test_version_and_device_probe():
     assert mk.device_count() >= 0  # 0 here (no GPU); never raises
 
 
+def source_digest():
+    """The Makefile's DIGEST: SHA-256 of csrc/*.hip|*.cpp|*.h and include/maxk_hip.h,
+    concatenated in C-locale order of their paths relative to spgemm-prunning_amd/."""
+    import glob
+    import hashlib
+    paths = [os.path.relpath(p, PKG) for pat in ("*.hip", "*.cpp", "*.h")
+             for p in glob.glob(os.path.join(PKG, "csrc", pat))]
+    paths.append(os.path.join("..", "include", "maxk_hip.h"))
+    h = hashlib.sha256()
+    for p in sorted(paths):
+        with open(os.path.join(PKG, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+@pytest.mark.skipif("MAXK_HIP_LIB" in os.environ, reason="a tuning variant is under test")
+def test_library_built_from_tree():
+    """The loaded libmaxk_hip.so was compiled from exactly the sources in this tree (the GPU
+    tests run whatever library is present, so a stale binary would otherwise go unnoticed)."""
+    from maxk_cuda_kernels import _capi
+    assert _capi.load().maxk_source_digest().decode() == source_digest()
+
+
 def test_host_side_argument_validation():
     from maxk_cuda_kernels import _capi
     L = _capi.load()
@@ -170,6 +193,7 @@ def test_pull_slice_rule():
     assert L.maxk_pull_slices(2_449_029, 256, 64) == 171
     assert L.maxk_pull_slices(4_000_000, 16, 64) == 62  # rows in a slice stay <= 65536
     gp = (232965 * 256 * 4 + 255) // 256 * 256
+    selq = 2 * ((232965 * 16 + 255) // 256 * 256)  # slot-ordered selectors + their l map
     assert L.maxk_sspmm_backward_pull_workspace_size(232965, 232965, 256, 16, 65) == \
-        gp + 65 * 228 * (16 << 10) * 4
+        gp + 65 * 228 * (16 << 10) * 4 + selq
     assert L.maxk_sspmm_backward_pull_workspace_size(10, 10, 0, 16, 1) == 0
