@@ -222,6 +222,8 @@ def main():
     ap.add_argument("--graph-dir", default=None,
                     help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
     ap.add_argument("--no-cpu-spmm", action="store_true")
+    ap.add_argument("--dist-mode", default="gather", choices=["gather", "halo"],
+                    help="N > 1: all-gather every CBSR row, or exchange only the halo rows")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -242,7 +244,13 @@ def main():
     # MAXK_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices, collectives
     # staged through host); the default is RCCL with one rank per GPU.
     backend = os.environ.get("MAXK_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
+    ndev = torch.cuda.device_count()  # does not initialise HIP on this image
+    if world > ndev:
+        # ranks share a device (the gloo rehearsal): more than two processes with HIP's
+        # default 4 hardware queues each stalled every rank's GPU work on the one-GPU box
+        # (tools/share_probe.py: 4 processes hung > 150 s in make_graph, finished in 0.3 s
+        # with GPU_MAX_HW_QUEUES=1), so each rank keeps one queue.  Set before HIP starts.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
     dev_idx = local_rank % ndev if backend == "gloo" else local_rank
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
@@ -269,9 +277,29 @@ def main():
         col = torch.from_numpy(g["indices"]).to(dev)
         V = g["v_num"]
         data = f"real graph {gdir}/{args.graph}.indptr|.indices; synthetic features"
-    else:
+    elif world == 1:
         row_ptr, col = maxk_graph.make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
         data = "synthetic"
+    else:
+        # one rank builds the graph, the others receive it (one broadcast of row_ptr + col)
+        cdev = dev if backend == "nccl" else torch.device("cpu")
+        if rank == 0:
+            row_ptr, col = maxk_graph.make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
+            n_e = torch.tensor([col.numel()], dtype=torch.int64, device=cdev)
+        else:
+            n_e = torch.zeros(1, dtype=torch.int64, device=cdev)
+        dist.broadcast(n_e, 0)
+        if rank != 0:
+            row_ptr = torch.empty(V + 1, dtype=torch.int32, device=dev)
+            col = torch.empty(int(n_e), dtype=torch.int32, device=dev)
+        for t in (row_ptr, col):
+            if backend == "nccl":
+                dist.broadcast(t, 0)
+            else:
+                h = t.cpu()
+                dist.broadcast(h, 0)
+                t.copy_(h)
+        data = "synthetic (built on rank 0, broadcast)"
     E = col.numel()
     gen = torch.Generator(device=dev).manual_seed(123)  # kernels/main.cu:74-77 seed
     val = torch.rand(E, generator=gen, device=dev)
@@ -286,7 +314,8 @@ def main():
     # ---- shard by vertex range, balanced by nnz (maxk_dist: the module the gloo tests cover)
     if world > 1:
         import maxk_dist
-        shard = maxk_dist.ShardedMaxK(row_ptr, col, val, rank, world, device=dev)
+        shard = maxk_dist.ShardedMaxK(row_ptr, col, val, rank, world, device=dev,
+                                      mode=args.dist_mode)
         v0, v1, vmax, n_cols = shard.v0, shard.v1, shard.vmax, shard.n_cols
         l_row_ptr, l_col, l_val = shard.row_ptr, shard.col_idx, shard.values
         l_X = X[v0:v1]
@@ -339,7 +368,7 @@ def main():
         if ev:
             ev[2].record()
         if world > 1:
-            maxk_dist.reduce_scatter_rows(gs_loc, gs_all)
+            gs_loc[:nl] = shard.scatter_grad(gs_all)
 
     stage(f"backward plan ({args.bwd_mode}) {t_plan:.3f}s")
     for _ in range(args.warmup):
@@ -420,7 +449,9 @@ def main():
     if world > 1:
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
                       "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
-                      "rows_per_rank_max": vmax, "edges_this_rank0": El})
+                      "dist_mode": args.dist_mode, "rows_per_rank_max": vmax,
+                      "edges_this_rank0": El, "cols_this_rank0": n_cols,
+                      "exchange_bytes_rank0": shard.exchange_bytes(k)})
 
     if rank == 0 and world == 1:
         # CBSR encode (top-k) and the dense rocSPARSE SpMM denominator, outside the timed region

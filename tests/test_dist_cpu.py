@@ -2,8 +2,10 @@
 
 The HIP kernels are replaced by the oracle (test infrastructure) through the
 `kernels=` hook, so what is checked here is the distributed logic itself:
-nnz-balanced partition, column remap to the padded space, all-gather of the
-CBSR rows, reduce-scatter of the gradient partials, autograd plumbing.  Each
+nnz-balanced partition, column remap to the padded space ("gather" mode) or
+the halo ("halo" mode), all-gather / all-to-allv of the CBSR rows,
+reduce-scatter / all-to-allv + index_add of the gradient partials, autograd
+plumbing.  Each
 rank's slice must equal the 1-process oracle result (forward bit-exact: every
 output row is computed whole on its owner; backward within 1e-5 relative,
 since the reduce-scatter sums per-rank partials in a different order).
@@ -61,7 +63,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None):
+def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gather"):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -76,13 +78,14 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None):
 
         shard = maxk_dist.ShardedMaxK(torch.from_numpy(row_ptr), torch.from_numpy(col),
                                       torch.from_numpy(val), rank, world,
-                                      kernels=OracleKernels(), bounds=bounds)
+                                      kernels=OracleKernels(), bounds=bounds, mode=mode)
         v0, v1 = shard.v0, shard.v1
         div = torch.from_numpy(deg[v0:v1]) if use_div else None
         val_l = torch.from_numpy(tv[v0:v1]).requires_grad_(True)
         y = maxk_dist.sharded_maxk_spgemm(shard, val_l, torch.from_numpy(ti[v0:v1]), D, div)
         y.backward(torch.from_numpy(g[v0:v1]))
-        q.put((rank, v0, v1, y.detach().numpy(), val_l.grad.numpy(), shard.bounds))
+        q.put((rank, v0, v1, y.detach().numpy(), val_l.grad.numpy(), shard.bounds,
+               shard.exchange_bytes(k), shard.n_cols))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # surface the failure to the parent
@@ -90,11 +93,12 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None):
         raise
 
 
-def _run(world, V=400, D=64, k=8, seed=0, use_div=True, bounds=None):
+def _run(world, V=400, D=64, k=8, seed=0, use_div=True, bounds=None, mode="gather"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, V, D, k, seed, use_div, q, bounds))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, V, D, k, seed, use_div, q, bounds, mode))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -118,17 +122,19 @@ def _single(V, D, k, seed, use_div):
     return y, gs
 
 
+@pytest.mark.parametrize("mode", ["gather", "halo"])
 @pytest.mark.parametrize("world,use_div,bounds", [(2, True, None), (3, False, None),
                                                   (4, True, None),
                                                   (3, True, [0, 150, 150, 400])])
-def test_sharded_matches_single_process(world, use_div, bounds):
-    """The last case gives rank 1 no rows: it still joins both collectives with an all-padding
-    chunk, and the other ranks' results are unchanged."""
+def test_sharded_matches_single_process(world, use_div, bounds, mode):
+    """The last case gives rank 1 no rows: it still joins every collective (an all-padding
+    chunk in "gather" mode, empty splits in "halo" mode), and the other ranks' results are
+    unchanged."""
     V, D, k, seed = 400, 64, 8, 7
-    outs = _run(world, V, D, k, seed, use_div, bounds)
+    outs = _run(world, V, D, k, seed, use_div, bounds, mode)
     y_ref, gs_ref = _single(V, D, k, seed, use_div)
     covered = 0
-    for rank, v0, v1, y, gs, bounds in outs:
+    for rank, v0, v1, y, gs, bounds, xb, n_cols in outs:
         assert bounds[0] == 0 and bounds[-1] == V
         np.testing.assert_array_equal(y, y_ref[v0:v1])
         np.testing.assert_allclose(gs, gs_ref[v0:v1], rtol=1e-5, atol=BWD_ATOL)
@@ -166,6 +172,75 @@ def test_column_remap_single_rank():
     cols = col[e0:e1].astype(np.int64)
     owner = np.searchsorted(np.array(b[1:]), cols, side="right")
     np.testing.assert_array_equal(s1.col_idx.numpy(), owner * 80 + cols - np.array(b)[owner])
+
+
+def test_halo_exchange_smaller_on_local_graph():
+    """A graph with locality (each row's columns near the row): the halo mode moves only the
+    neighbouring shards' boundary rows, and its column space is the shard's halo."""
+    V, D, k, world = 600, 32, 4, 3
+    rng = np.random.default_rng(4)
+    deg = rng.poisson(5, V).astype(np.int64)
+    row_ptr = np.zeros(V + 1, np.int64)
+    np.cumsum(deg, out=row_ptr[1:])
+    rows = np.repeat(np.arange(V), deg)
+    col = np.clip(rows + rng.integers(-20, 21, rows.size), 0, V - 1).astype(np.int32)
+    val = rng.random(col.size, dtype=np.float32)
+    args = (torch.from_numpy(row_ptr.astype(np.int32)), torch.from_numpy(col),
+            torch.from_numpy(val))
+    outs = _run_local(world, args, D, k)  # each rank also checks halo == gather results
+    for rank, v0, v1, y, gs, bounds, xb_halo, n_cols, xb_gather in outs:
+        assert xb_halo["fwd_recv"] < xb_gather["fwd_recv"] / 4  # boundary rows only
+        e0, e1 = row_ptr[v0], row_ptr[v1]
+        assert n_cols == np.unique(col[e0:e1]).size
+
+
+def _local_worker(rank, world, port, args, D, k, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        rp, col, val = args
+        V = rp.numel() - 1
+        rng = np.random.default_rng(9)
+        tv, ti = oracle.topk(rng.standard_normal((V, D)).astype(np.float32), k)
+        g = rng.standard_normal((V, D)).astype(np.float32)
+        res = {}
+        for mode in ("gather", "halo"):
+            shard = maxk_dist.ShardedMaxK(rp, col, val, rank, world, kernels=OracleKernels(),
+                                          mode=mode)
+            v0, v1 = shard.v0, shard.v1
+            val_l = torch.from_numpy(tv[v0:v1]).requires_grad_(True)
+            y = maxk_dist.sharded_maxk_spgemm(shard, val_l, torch.from_numpy(ti[v0:v1]), D)
+            y.backward(torch.from_numpy(g[v0:v1]))
+            res[mode] = (y.detach().numpy(), val_l.grad.numpy(), shard.exchange_bytes(k),
+                         shard.n_cols)
+        yg, gg, xg, _ = res["gather"]
+        yh, gh, xh, nh = res["halo"]
+        np.testing.assert_array_equal(yh, yg)
+        np.testing.assert_allclose(gh, gg, rtol=1e-5, atol=BWD_ATOL)
+        q.put((rank, v0, v1, yh, gh, shard.bounds, xh, nh, xg))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, "error", repr(e)))
+        raise
+
+
+def _run_local(world, args, D, k):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_worker, args=(r, world, port, args, D, k, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for o in outs:
+        assert o[1] != "error", o
+    return sorted(outs, key=lambda o: o[0])
 
 
 @pytest.mark.gpu

@@ -1,0 +1,112 @@
+"""GPU: the sharded aggregation (maxk_dist) at world size 2 and 4 with the HIP kernels, on
+the box's one MI355X (BASELINE.json configs[3], rehearsed on one device).
+
+The parent writes a products-shaped graph (power-law degrees around 50, D = 256, k = 32),
+starts N fresh worker processes (tests/dist_gpu_worker.py: gloo collectives staged through
+host memory, HIP kernels on cuda:0, one hardware queue per process) and checks every rank's
+forward rows and CBSR-gradient rows, in both exchange modes ("gather" and "halo"), against
+the 1-process HIP result (1e-5 relative: hub rows split differently over work items, and the
+gradient partials are summed in another order) and against the oracle (1e-4, north_star).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def products_like(V, avg, seed):
+    """Power-law out-degrees (mean ~avg), random sorted distinct columns, self loops."""
+    rng = np.random.default_rng(seed)
+    w = (np.arange(V) + 30.0) ** -0.75
+    deg = np.minimum(rng.poisson(avg * w / w.mean()), V - 1) + 1
+    rows, cols = [], []
+    for r in range(V):
+        c = rng.choice(V, int(deg[r]), replace=False)
+        c[0] = r  # a self loop per row
+        cols.append(np.unique(c))
+    row_ptr = np.zeros(V + 1, np.int64)
+    np.cumsum([c.size for c in cols], out=row_ptr[1:])
+    return row_ptr.astype(np.int32), np.concatenate(cols).astype(np.int32)
+
+
+@pytest.fixture(scope="module")
+def graph(tmp_path_factory):
+    V, D, k = 12000, 256, 32
+    row_ptr, col = products_like(V, 50, 3)
+    rng = np.random.default_rng(4)
+    g = {"row_ptr": row_ptr, "col": col, "val": rng.random(col.size, dtype=np.float32),
+         "x": rng.standard_normal((V, D), dtype=np.float32),
+         "g": rng.standard_normal((V, D), dtype=np.float32),
+         "deg": np.maximum(np.diff(row_ptr), 1).astype(np.float32), "k": k, "D": D}
+    d = tmp_path_factory.mktemp("dist_gpu")
+    np.savez(d / "graph.npz", **g)
+    return d, g
+
+
+@pytest.fixture(scope="module")
+def single(graph, cuda):
+    """The 1-process HIP result and the oracle, over the whole graph."""
+    import maxk_cuda_kernels as mk
+    _, g = graph
+    to = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
+    k, D = g["k"], g["D"]
+    cv, ci = mk.topk_cbsr(to(g["x"]), k)
+    rp, cl, va, dg = to(g["row_ptr"]), to(g["col"]), to(g["val"]), to(g["deg"])
+    y = mk.spgemm_forward(rp, cl, va, cv, ci, D, row_div=dg).cpu().numpy()
+    gs = mk.sspmm_backward(rp, cl, va, to(g["g"]), ci, row_div=dg).cpu().numpy()
+    cvn, cin = cv.cpu().numpy(), ci.cpu().numpy()
+    yo = O.spgemm_fwd(g["row_ptr"], g["col"], g["val"], cvn, cin, D, row_div=g["deg"])
+    go = O.sspmm_bwd(g["row_ptr"], g["col"], g["val"], g["g"], cin, row_div=g["deg"])
+    return y, gs, yo, go
+
+
+def close(a, ref, tol):
+    err = np.abs(a.astype(np.float64) - ref.astype(np.float64))
+    bad = err > tol * np.maximum(1.0, np.abs(ref.astype(np.float64)))
+    assert not bad.any(), f"{bad.sum()} elements off; max err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_world_n_on_one_gpu(graph, single, world):
+    d, g = graph
+    y1, gs1, yo, go = single
+    port = _free_port()
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_gpu_worker.py"), str(d),
+                               str(r), str(world), str(port)], env=env)
+             for r in range(world)]
+    try:
+        rcs = [p.wait(timeout=100) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0] * world, rcs
+    V = g["row_ptr"].size - 1
+    for mode in ("gather", "halo"):
+        covered = 0
+        for r in range(world):
+            with np.load(os.path.join(d, f"rank{r}.npz"), allow_pickle=False) as z:
+                b = z[f"{mode}_bounds"]
+                v0, v1 = int(b[r]), int(b[r + 1])
+                close(z[f"{mode}_y"], y1[v0:v1], 1e-5)
+                close(z[f"{mode}_gs"], gs1[v0:v1], 1e-5)
+                close(z[f"{mode}_y"], yo[v0:v1], 1e-4)
+                close(z[f"{mode}_gs"], go[v0:v1], 1e-4)
+                covered += v1 - v0
+        assert covered == V
