@@ -12,7 +12,7 @@ BENCH="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-rocsparse"
 STEPS=${STEPS:-tests,smoke,bench,stats,pmc}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 if has tests; then
-  timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
   tail -3 $O/pytest_gpu.log
 fi
 if has smoke; then
