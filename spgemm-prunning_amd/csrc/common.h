@@ -57,6 +57,9 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_U  // pull_tile_kernel: wave instructions of entries per step
 #define MAXK_PULL_U 4
 #endif
+#ifndef MAXK_PULL_QU  // pull_q_kernel: wave instructions of entries per step (U=2 vs 4: Reddit
+#define MAXK_PULL_QU 2   // k=8 1.53 vs 1.62 ms, k=32 3.60 vs 3.80, k=16 equal)
+#endif
 #ifndef MAXK_PULL_Q  // pull, k % 4 == 0: quantile-slot selectors + pipelined pull_q_kernel
 #define MAXK_PULL_Q 1
 #endif
@@ -65,6 +68,12 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #endif
 #ifndef MAXK_PULL_MIN_KP  // pull_q_kernel: fewest slots per destination a part may keep
 #define MAXK_PULL_MIN_KP 16
+#endif
+#ifndef MAXK_PULL_ABL  // tuning only (wrong results): 1 no gathers, 2 no LDS adds, 4 row 0, 8 fixed columns
+#define MAXK_PULL_ABL 0
+#endif
+#ifndef MAXK_PULL_TRANSPOSE  // pull_q_kernel: a quarter's entries interleaved across its quads
+#define MAXK_PULL_TRANSPOSE 1
 #endif
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1

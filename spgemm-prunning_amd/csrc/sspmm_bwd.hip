@@ -784,7 +784,17 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
     constexpr int NL = (STEP + kWave - 1) / kWave;  // entry loads per step (one per lane)
     const int tid = threadIdx.x;
     const int lane = lane_id(), w = tid / kWave;
-    const int g = lane / LR, q = lane % LR;
+    // Lane -> (entry g, lane-in-entry q).  The texture path serves a 16-lane quarter in four
+    // lane columns {c, c+4, c+8, c+12}, and lanes of one cache line that sit in one quad
+    // cost extra cycles (tools/ta_probe.hip, L1-resident: 4 lines per quarter cost 4.2
+    // cycles spread one lane per quad, 8.7 with a quad per line).  An entry's lanes gather
+    // neighbouring sorted columns, often one line, so with LR < 16 a quarter's entries are
+    // interleaved: lane j of the quarter takes entry j % EPQ and lane-in-entry j / EPQ.
+    constexpr int EPQ = LR < 16 ? 16 / LR : 1;  // entries per 16-lane quarter
+    const int g = MAXK_PULL_TRANSPOSE && LR < 16
+                      ? (lane / 16) * EPQ + (lane % 16) % EPQ
+                      : lane / LR;
+    const int q = MAXK_PULL_TRANSPOSE && LR < 16 ? (lane % 16) / EPQ : lane % LR;
     const bool qok = q < kp / 4;
     const int ks = kp + 1;
     const int H = k / kp;
@@ -865,23 +875,34 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t ro = ok[u] ? (ex[u] & 0xffffu) * Db : 0x80000000u;
+            uint32_t ro = ok[u] ? (ex[u] & 0xffffu) * Db : 0x80000000u;
+            if ((MAXK_PULL_ABL & 4) && ok[u]) ro = 0;  // tuning: every entry reads row 0
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const uint32_t c = (sv[u] >> (8 * i)) & 255u;
+                uint32_t c = (sv[u] >> (8 * i)) & 255u;
+                if (MAXK_PULL_ABL & 8) c = 16 * i + 4 * q;  // tuning: 16 contiguous columns
                 uint32_t off = ro + c * 4u;
                 if (!FULLD) off = c < (uint32_t)D ? off : 0x80000000u;  // past the buffer: 0
-                v[u][i] = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(grs, (int)off, 0, 0));
+                if (MAXK_PULL_ABL & 1)
+                    v[u][i] = (float)c;
+                else
+                    v[u][i] = __builtin_bit_cast(
+                        float, __builtin_amdgcn_raw_buffer_load_b32(grs, (int)off, 0, 0));
             }
         }
     };
+    float abl_sum = 0.f;
     auto consume = [&](float(&v)[U][4], int(&dc)[U], float(&wc)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             double *a = &acc[dc[u]];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) atomicAdd(a + i, (double)(wc[u] * v[u][i]));
+            for (int i = 0; i < 4; ++i) {
+                if (MAXK_PULL_ABL & 2)
+                    abl_sum += wc[u] * v[u][i] * (float)dc[u];
+                else
+                    atomicAdd(a + i, (double)(wc[u] * v[u][i]));
+            }
         }
     };
     if (nsteps > 0) {
@@ -905,6 +926,7 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+    if (MAXK_PULL_ABL & 2) acc[idle] = abl_sum;
     __syncthreads();
     // tile_out[t] is [2^shift, k] in slot order; part h fills slots [h * kp, (h + 1) * kp)
     float *o = tile_out + (size_t)t * ((size_t)k << shift) + h * kp;
@@ -1397,12 +1419,12 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
         switch (lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
 #define MAXK_CASE(LRV)                                                                        \
     case LRV * 2 + 1:                                                                         \
-        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_U, true>), dim3(grid), dim3(1024),    \
+        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, true>), dim3(grid), dim3(1024),    \
                            lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
                            (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
         break;                                                                                \
     case LRV * 2:                                                                             \
-        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_U, false>), dim3(grid), dim3(1024),   \
+        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, false>), dim3(grid), dim3(1024),   \
                            lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
                            (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
         break;
