@@ -69,7 +69,7 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_MIN_KP  // pull_q_kernel: fewest slots per destination a part may keep
 #define MAXK_PULL_MIN_KP 16
 #endif
-#ifndef MAXK_PULL_ABL  // tuning only (wrong results): 1 no gathers, 2 no LDS adds, 4 row 0, 8 fixed columns
+#ifndef MAXK_PULL_ABL  // tuning only (wrong results): 1 no gathers, 2 no LDS adds, 4 row 0, 8 fixed columns, 16 no entries
 #define MAXK_PULL_ABL 0
 #endif
 #ifndef MAXK_PULL_TRANSPOSE  // pull_q_kernel: a quarter's entries interleaved across its quads

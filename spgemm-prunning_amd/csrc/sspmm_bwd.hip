@@ -772,13 +772,13 @@ __global__ __launch_bounds__(kBlock) void pull_sel_kernel(const uint8_t *__restr
 //  * tiles in XCD order (MAXK_PULL_XCD): XCD x runs the x-th eighth of the tile sequence
 //    in order, so each XCD's L2 holds the one slice it works on instead of every XCD
 //    pulling every slice.
+// One tile's entry loop of pull_q_kernel: adds the tile's n_e entries (ers)
+// into the fp64 accumulator, gathering from the slice's G' rows (grs).
 template <int LR, int U, bool FULLD>
-__global__ __launch_bounds__(1024) void pull_q_kernel(
-    const float *__restrict__ Gp, const uint8_t *__restrict__ sel_q,
-    const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
-    float *__restrict__ tile_out, int64_t num_cols, int n_buckets, int n_tiles,
-    int rows_per_slice, int64_t num_rows, int D, int k, int kp, int shift) {
-    extern __shared__ double acc[];  // [(kp + 1) << shift], then [kp << shift] selector bytes
+__device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_lds,
+                                               __amdgpu_buffer_rsrc_t grs,
+                                               __amdgpu_buffer_rsrc_t ers, int n_e, int D,
+                                               int kp, int shift) {
     constexpr int EPI = kWave / LR;                 // entries per wave instruction
     constexpr int STEP = EPI * U;                   // entries per wave step
     constexpr int NL = (STEP + kWave - 1) / kWave;  // entry loads per step (one per lane)
@@ -797,47 +797,16 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
     const int q = MAXK_PULL_TRANSPOSE && LR < 16 ? (lane % 16) / EPQ : lane % LR;
     const bool qok = q < kp / 4;
     const int ks = kp + 1;
-    const int H = k / kp;
-    const int tp = MAXK_PULL_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    if (tp >= n_tiles * H) return;  // the XCD grid's padding
-    const int t = tp / H, h = tp % H;
-    const int j = t % n_buckets;
-    const int64_t r0 = (int64_t)(t / n_buckets) * rows_per_slice;
-    const int64_t nrows = num_rows - r0 < rows_per_slice ? num_rows - r0 : rows_per_slice;
-    const float *__restrict__ Gs = Gp + r0 * D;
-    const int s0 = tile_ptr[t], s1 = tile_ptr[t + 1];
-    const int64_t c0 = (int64_t)j << shift;
-    uint8_t *sel_lds = reinterpret_cast<uint8_t *>(acc + (ks << shift));
-    for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
-    {  // part h of each destination's slot-ordered selectors: kp bytes of its k-byte row
-        const uint8_t *__restrict__ selg = sel_q + c0 * k + h * kp;
-        const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
-        if (kp == k) {
-            const int nb = rows * k;  // c0 * k is a multiple of 16 (shift >= 4), as is sel_lds
-            for (int i = tid; i < nb / 16; i += 1024)
-                reinterpret_cast<uint4 *>(sel_lds)[i] = reinterpret_cast<const uint4 *>(selg)[i];
-            for (int i = (nb & ~15) + tid; i < nb; i += 1024) sel_lds[i] = selg[i];
-        } else {  // kp % 4 == 0: 4-byte words
-            const int wpr = kp / 4;
-            for (int i = tid; i < rows * wpr; i += 1024)
-                reinterpret_cast<uint32_t *>(sel_lds)[i] =
-                    *reinterpret_cast<const uint32_t *>(selg + (i / wpr) * k + (i % wpr) * 4);
-        }
-    }
-    __syncthreads();
-    const auto grs = wave_buffer(Gs, (uint32_t)(nrows > 0 ? nrows : 0) * (uint32_t)D * 4u);
-    const auto ers = wave_buffer(ent + s0, (uint32_t)(s1 - s0) * 8u);
     const uint32_t Db = (uint32_t)D * 4u;
     const int stride = 16 * STEP;  // 16 waves
-    const int base = w * STEP;     // entry offsets relative to s0
-    const int n_e = s1 - s0;
+    const int base = w * STEP;     // entry offsets relative to the tile's first entry
     // Every step is issued the same way: no load sits under a branch, since the compiler
     // merges the counters of the two sides of a branch conservatively and then waits for
     // loads it could leave in flight.  Entries past the tile read 0 (past the descriptor),
     // their gathers get offsets past the G' descriptor (0, no memory access), their weight
     // 0, and their adds (+0.0) go to a lane-private row of the accumulator.  The loop runs
     // an even number of steps; the last issue is never consumed.
-    const int nsteps = base < n_e ? (n_e - base + stride - 1) / stride : 0;
+    const int nsteps = base < n_e && !(MAXK_PULL_ABL & 16) ? (n_e - base + stride - 1) / stride : 0;
     const int idle = (w * kWave + lane) & ((1 << shift) - 1);
 
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -927,16 +896,134 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
         }
     }
     if (MAXK_PULL_ABL & 2) acc[idle] = abl_sum;
-    __syncthreads();
-    // tile_out[t] is [2^shift, k] in slot order; part h fills slots [h * kp, (h + 1) * kp)
+}
+
+// Where tile t's pieces live: its slice's first row and row count, its bucket's first column.
+struct PullTile {
+    int64_t r0, nrows, c0;
+    int s0, s1;
+};
+__device__ __forceinline__ PullTile pull_tile_of(int t, const int32_t *__restrict__ tile_ptr,
+                                                 int n_buckets, int rows_per_slice,
+                                                 int64_t num_rows, int shift) {
+    PullTile p;
+    p.r0 = (int64_t)(t / n_buckets) * rows_per_slice;
+    p.nrows = num_rows - p.r0 < rows_per_slice ? num_rows - p.r0 : rows_per_slice;
+    p.c0 = (int64_t)(t % n_buckets) << shift;
+    p.s0 = tile_ptr[t];
+    p.s1 = tile_ptr[t + 1];
+    return p;
+}
+
+// Part h of each destination's slot-ordered selectors (kp bytes of its k-byte row) for the
+// bucket starting at column c0, loaded to registers (up to kSelRegs 16-B pieces per
+// thread) and then stored to LDS.
+constexpr int kSelRegs = 2;
+struct PullSel {
+    uint4 v[kSelRegs];
+};
+__device__ __forceinline__ PullSel pull_sel_load(const uint8_t *__restrict__ sel_q, int64_t c0,
+                                                 int64_t num_cols, int k, int kp, int h,
+                                                 int shift) {
+    PullSel r;
+    const int tid = threadIdx.x;
+    const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
+    const uint8_t *__restrict__ selg = sel_q + c0 * k + h * kp;
+    // piece i: destination i / ppr, bytes [16 * (i % ppr), +16) of its kp (ppr = kp / 16), or
+    // for kp < 16 whole 16-B groups of 16 / kp destinations packed from their kp-byte parts
+#pragma unroll
+    for (int m = 0; m < kSelRegs; ++m) {
+        const int i = tid + m * 1024;
+        uint4 x = make_uint4(0u, 0u, 0u, 0u);
+        if (kp % 16 == 0) {
+            const int ppr = kp / 16;
+            if (i < rows * ppr)
+                x = *reinterpret_cast<const uint4 *>(selg + (int64_t)(i / ppr) * k + (i % ppr) * 16);
+        } else {  // kp % 16 != 0 (kp % 4 == 0): 4-byte words, 4 per piece
+            uint32_t wd[4];
+            const int wpr = kp / 4;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int wi = i * 4 + b;
+                wd[b] = wi < rows * wpr
+                            ? *reinterpret_cast<const uint32_t *>(selg + (int64_t)(wi / wpr) * k +
+                                                                  (wi % wpr) * 4)
+                            : 0u;
+            }
+            x = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        }
+        r.v[m] = x;
+    }
+    return r;
+}
+__device__ __forceinline__ void pull_sel_store(uint8_t *sel_lds, const PullSel &r, int kp,
+                                               int shift) {
+    const int n16 = (kp << shift) / 16;
+#pragma unroll
+    for (int m = 0; m < kSelRegs; ++m) {
+        const int i = threadIdx.x + m * 1024;
+        if (i < n16) reinterpret_cast<uint4 *>(sel_lds)[i] = r.v[m];
+    }
+}
+
+// tile_out[t] is [2^shift, k] in slot order; part h fills slots [h * kp, (h + 1) * kp).
+__device__ __forceinline__ void pull_flush(const double *acc, float *__restrict__ tile_out, int t,
+                                           int h, int k, int kp, int shift) {
+    const int ks = kp + 1;
     float *o = tile_out + (size_t)t * ((size_t)k << shift) + h * kp;
     const int w4 = kp / 4;
-    for (int i4 = tid; i4 < (kp << shift) / 4; i4 += 1024) {
+    for (int i4 = threadIdx.x; i4 < (kp << shift) / 4; i4 += 1024) {
         const int c = i4 / w4, s4 = i4 % w4;
         const double *a = &acc[c * ks + 4 * s4];
         *reinterpret_cast<float4 *>(o + (size_t)c * k + 4 * s4) =
             make_float4((float)a[0], (float)a[1], (float)a[2], (float)a[3]);
     }
+}
+
+// Parts: with H = k / kp parts, destination c's slots split by sorted position into H
+// groups of kp (part h: the h-th kp smallest selectors), and one workgroup sums one part of
+// one tile: the accumulator holds kp slots per destination, so a bucket holds H times the
+// destinations and a source row meets ~H times fewer buckets; each part's gathers cover
+// only its share of a row's columns (the h-th kp order statistics of every entry).  The
+// tile's entries are read H times.  Model of the Reddit stream (k = 16): L2 lines per entry
+// 3.2 -> 2.3 at H = 2.
+// One 1024-thread workgroup per (tile, part), as pull_tile_kernel (fp64 LDS accumulator of
+// the bucket, its slot-ordered selector rows copied next to it), with:
+//  * quantile slots (above): lane q's u32 selector word holds its four instructions'
+//    columns;
+//  * a two-step software pipeline: step n's gathers are issued before step n-1's adds, and
+//    the entries two steps ahead, so a wave keeps 2 x 4U gathers in flight and never waits
+//    on loads it has just issued (the one-step loop waited for every load at its head);
+//  * the G' gathers through a wave-uniform buffer descriptor over the slice's rows with
+//    32-bit offsets (no 64-bit address math per value); a selector >= D (possible only
+//    when D < 256, !FULLD) gets an offset past the descriptor, and the hardware returns 0;
+//  * tiles in XCD order (MAXK_PULL_XCD): XCD x runs the x-th eighth of the tile sequence
+//    in order, so each XCD's L2 holds the one slice it works on instead of every XCD
+//    pulling every slice.
+template <int LR, int U, bool FULLD>
+__global__ __launch_bounds__(1024) void pull_q_kernel(
+    const float *__restrict__ Gp, const uint8_t *__restrict__ sel_q,
+    const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
+    float *__restrict__ tile_out, int64_t num_cols, int n_buckets, int n_tiles,
+    int rows_per_slice, int64_t num_rows, int D, int k, int kp, int shift) {
+    extern __shared__ double acc[];  // [(kp + 1) << shift], then [kp << shift] selector bytes
+    const int tid = threadIdx.x;
+    const int ks = kp + 1;
+    const int H = k / kp;
+    const int tp = MAXK_PULL_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    if (tp >= n_tiles * H) return;  // the XCD grid's padding
+    const int t = tp / H, h = tp % H;
+    const PullTile p = pull_tile_of(t, tile_ptr, n_buckets, rows_per_slice, num_rows, shift);
+    uint8_t *sel_lds = reinterpret_cast<uint8_t *>(acc + (ks << shift));
+    for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
+    pull_sel_store(sel_lds, pull_sel_load(sel_q, p.c0, num_cols, k, kp, h, shift), kp, shift);
+    __syncthreads();
+    const auto grs =
+        wave_buffer(Gp + p.r0 * D, (uint32_t)(p.nrows > 0 ? p.nrows : 0) * (uint32_t)D * 4u);
+    const auto ers = wave_buffer(ent + p.s0, (uint32_t)(p.s1 - p.s0) * 8u);
+    pull_q_entries<LR, U, FULLD>(acc, sel_lds, grs, ers, p.s1 - p.s0, D, kp, shift);
+    __syncthreads();
+    pull_flush(acc, tile_out, t, h, k, kp, shift);
 }
 
 // grad_cbsr rows of bucket j = the sum of its slices' tiles, in slice order.  With lmap
@@ -1414,17 +1501,17 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
                            0, s, cbsr_idx, sel_q, lm, num_cols, k, kp);
         MAXK_LAUNCHED("pull_sel_kernel");
         const int64_t work = (int64_t)tiles * parts;
-        const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);
         const bool fulld = dim_origin == kMaxDim;
+        const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);
         switch (lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
 #define MAXK_CASE(LRV)                                                                        \
     case LRV * 2 + 1:                                                                         \
-        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, true>), dim3(grid), dim3(1024),    \
+        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, true>), dim3(grid), dim3(1024),   \
                            lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
                            (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
         break;                                                                                \
     case LRV * 2:                                                                             \
-        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, false>), dim3(grid), dim3(1024),   \
+        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, false>), dim3(grid), dim3(1024),  \
                            lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
                            (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
         break;
