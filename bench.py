@@ -41,7 +41,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 OP_KERNELS = {
     "spgemm_forward": ["cbsr_pack_kernel", "spgemm_fwd_kernel", "slab_fixup_kernel<0>"],
     "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>"],
-    "sspmm_backward_pull": ["pull_tile_kernel", "pull_reduce_kernel"],  # + gprime_kernel with row_div
+    # k % 4 == 0: slot-ordered selectors, quantile-slot tiles; else pull_tile_kernel; plus
+    # gprime_kernel when a row_div is given (the bench passes none)
+    "sspmm_backward_pull": ["pull_sel_kernel", "pull_q_kernel", "pull_tile_kernel",
+                            "pull_reduce_kernel", "gprime_kernel"],
     "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
 }

@@ -417,6 +417,37 @@ def test_duplicate_selectors_accumulate(mk, cuda):
     close(gs, go)
 
 
+def test_selectors_past_D_read_zero(mk, cuda):
+    """A selector >= D (possible when D < 256; the reference does no bounds check,
+    cuda_kernel_bindings.cpp:106-161) contributes nothing, in the forward and in every
+    backward mode: D = 100 with selector 200 on the last row (whose G row ends the
+    allocation) and on random other rows.  Expected: the oracle on G padded with zero
+    columns to 256 (backward) and on the full-width forward cut back to D."""
+    rng = np.random.default_rng(21)
+    V, D, k = 300, 100, 16
+    row_ptr, col = rand_graph(rng, V, 30, hubs=((V - 1, 250),))
+    val = rng.random(col.size, dtype=np.float32)
+    cv, ci = O.topk(rng.standard_normal((V, D), dtype=np.float32), k)
+    ci[V - 1, 3] = 200
+    bad = rng.choice(V - 1, 40, replace=False)
+    ci[bad, rng.integers(0, k, 40)] = rng.integers(D, 256, 40).astype(np.uint8)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    g_pad = np.zeros((V, 256), np.float32)
+    g_pad[:, :D] = g
+    go = O.sspmm_bwd(row_ptr, col, val, g_pad, ci)
+    yo = O.spgemm_fwd(row_ptr, col, val, cv, ci, 256)[:, :D]
+    y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda),
+                          T(ci, cuda), D, validate=False)
+    close(y, yo)
+    for mode in ("pull", "bucket", "csc", "atomic"):
+        gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
+                               T(ci, cuda), mode=mode, validate=False)
+        close(gs, go)
+    with pytest.raises(RuntimeError):  # and the validating call rejects the input
+        mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
+                          T(ci, cuda), validate=True)
+
+
 def test_rectangular_shard(mk, cuda):
     """num_rows != num_cols: a vertex-range shard's rows against the full CBSR."""
     rng = np.random.default_rng(11)

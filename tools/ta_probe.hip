@@ -45,14 +45,14 @@ __constant__ uint16_t c_pat[64];  // MODE 5: lane -> (line id << 8 | dword offse
 // 5: dword gather by the lane pattern c_pat (line ids made random per instruction)
 template <int MODE>
 __global__ __launch_bounds__(256) void probe(const float *__restrict__ T, int iters, int N,
-                                             float *out, uint32_t lmask) {
+                                             float *out, uint32_t lmask, int shared) {
     const int lane = threadIdx.x % 64;
     const uint32_t wave = (blockIdx.x * 4 + threadIdx.x / 64);
-    const float *Tb = T + (size_t)(blockIdx.x % 8) * (kTableBytes / 4);
-    const auto rs = make_rsrc(Tb, kTableBytes);
+    const float *Tb = T + (shared ? 0 : (size_t)(blockIdx.x % 8) * (lmask + 1) * 32);
+    const auto rs = make_rsrc(Tb, (lmask + 1) * 128);
     float acc = 0.f;
-    const int grp = lane % N;         // lane's line within the instruction
-    const int pos = lane / N;         // lane's slot within its line
+    const int grp = MODE >= 6 ? lane / (64 / N) : lane % N;  // lane's line in the instruction
+    const int pos = MODE >= 6 ? lane % (64 / N) : lane / N;  // lane's slot within its line
     const uint32_t gmul = (uint32_t)(MODE == 5 ? (c_pat[lane] >> 8) : grp) * 2654435761u;
     const uint32_t poff = c_pat[lane] & 255u;
     for (int it = 0; it < iters; ++it) {
@@ -61,7 +61,12 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ T, int it
         for (int u = 0; u < U; ++u) {
             const uint32_t seed = hash32(wave * 7919u + (uint32_t)(it * U + u) * 104729u);
             const uint32_t line = ((seed + gmul) >> 7) & lmask;
-            if (MODE == 5) {
+            if (MODE == 6) {  // x4, consecutive lanes per line (a record read whole)
+                const f32x4 x = *reinterpret_cast<const f32x4 *>(Tb + line * 32 + (pos * 4) % 32);
+                v[u] = x.x + x.y + x.z + x.w;
+            } else if (MODE == 7) {  // dword, consecutive lanes per line
+                v[u] = Tb[line * 32 + pos % 32];
+            } else if (MODE == 5) {
                 v[u] = Tb[line * 32 + poff];
             } else if (MODE == 0) {
                 v[u] = Tb[line * 32 + (pos * 4) % 32];
@@ -88,11 +93,12 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ T, int it
 
 int main(int argc, char **argv) {
     const uint32_t lmask = (argc > 1 ? (uint32_t)atoi(argv[1]) : (uint32_t)kLines) - 1;  // table lines
-    printf("table %u lines of 128 B per XCD\n", lmask + 1);
+    const int shared = argc > 2 ? atoi(argv[2]) : 0;  // 1: one table for all XCDs
+    printf("table %u lines of 128 B %s\n", lmask + 1, shared ? "shared by all XCDs" : "per XCD");
     float *T, *out;
-    CK(hipMalloc(&T, (size_t)8 * kTableBytes));
+    CK(hipMalloc(&T, (size_t)8 * (lmask + 1) * 128));
     CK(hipMalloc(&out, 64));
-    CK(hipMemset(T, 0, (size_t)8 * kTableBytes));
+    CK(hipMemset(T, 0, (size_t)8 * (lmask + 1) * 128));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
@@ -113,12 +119,16 @@ int main(int argc, char **argv) {
                cyc / n);
     };
     for (int n : {1, 2, 4, 8, 16, 32, 64}) {
-        t("gather", n, [&] { probe<0><<<wgs, 256>>>(T, iters, n, out, lmask); });
-        t("gatherb", n, [&] { probe<1><<<wgs, 256>>>(T, iters, n, out, lmask); });
-        t("x2", n, [&] { probe<2><<<wgs, 256>>>(T, iters, n, out, lmask); });
-        t("x4", n, [&] { probe<3><<<wgs, 256>>>(T, iters, n, out, lmask); });
+        t("gather", n, [&] { probe<0><<<wgs, 256>>>(T, iters, n, out, lmask, shared); });
+        t("gatherb", n, [&] { probe<1><<<wgs, 256>>>(T, iters, n, out, lmask, shared); });
+        t("x2", n, [&] { probe<2><<<wgs, 256>>>(T, iters, n, out, lmask, shared); });
+        t("x4", n, [&] { probe<3><<<wgs, 256>>>(T, iters, n, out, lmask, shared); });
     }
-    t("row1k", 8, [&] { probe<4><<<wgs, 256>>>(T, iters, 8, out, lmask); });
+    t("row1k", 8, [&] { probe<4><<<wgs, 256>>>(T, iters, 8, out, lmask, shared); });
+    for (int n : {4, 8, 16}) {  // records: 64 / n consecutive lanes per random line
+        t("rec_x4", n, [&] { probe<6><<<wgs, 256>>>(T, iters, n, out, lmask, shared); });
+        t("rec_dw", n, [&] { probe<7><<<wgs, 256>>>(T, iters, n, out, lmask, shared); });
+    }
     // quarter patterns (16 lanes each; j = lane % 16, q = lane / 16):
     //  P2: 4 lines x both 64-B halves per quarter   P3: 8 lines, first half only
     //  P4: 2 lines x both halves                    P5: 8 lines x both halves (16 segments)
@@ -150,7 +160,7 @@ int main(int argc, char **argv) {
         CK(hipMemcpyToSymbol(HIP_SYMBOL(c_pat), pat, sizeof pat));
         char nm[16];
         snprintf(nm, sizeof nm, "P%d", pid);
-        t(nm, pid, [&] { probe<5><<<wgs, 256>>>(T, iters, 1, out, lmask); });
+        t(nm, pid, [&] { probe<5><<<wgs, 256>>>(T, iters, 1, out, lmask, shared); });
     }
     return 0;
 }
