@@ -10,7 +10,7 @@ cp $O/stats_bench.json $P/stats_bench/bench.json
 cp $O/bench.json $P/bench_default.json
 cp $O/pmc_fetch/run_counter_collection.csv $P/pmc_fetch_size.csv
 cp $O/pmc_write/run_counter_collection.csv $P/pmc_write_size.csv
-cp $O/pytest_gpu.log $P/pytest_gpu.log
+[ -f $O/pytest_gpu.log ] && cp $O/pytest_gpu.log $P/pytest_gpu.log
 rm -f $P/traffic.json
 python tools/pmc_summary.py $P/pmc_fetch_size.csv $P/pmc_write_size.csv --traffic-out $P/traffic.json --key $KEY > $P/pmc_summary.txt
 python tools/stats_summary.py $P/stats_bench/kernel_stats.csv $P/stats_bench/bench.json > $P/kernel_stats_summary.txt
