@@ -29,6 +29,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_BWD_U
 #define MAXK_BWD_U 8
 #endif
+#ifndef MAXK_FWD_SHORT  // forward: rows of at most this many edges go in batches of 64/KG
+#define MAXK_FWD_SHORT 16  // (one row per lane group); 0 = off
+#endif
 #ifndef MAXK_FWD_WAVES
 #define MAXK_FWD_WAVES 1
 #endif

@@ -117,6 +117,53 @@ template <int KG, int U, bool WIDE>
 struct EdgeWalker {
     static constexpr int G = kWave / KG;  // edges per wave step
 
+    // Short-row batch: group g (KG lanes) walks row g's edges [sb_g, se_g) alone, U at a
+    // time, into its own copy acc_g; the rows are consecutive, so their edges are one
+    // contiguous range [e0, e_end) and one descriptor covers every group.  Edges past a
+    // group's row (the next row's, or past e_end: 0) go to the trash column with weight 0.
+    __device__ __forceinline__ static void run_rows(float *acc_g, const int32_t *__restrict__ col_idx,
+                                                    const float *__restrict__ edge_val,
+                                                    const uint8_t *__restrict__ rec, int RS,
+                                                    int e0, int e_end, int sb_g, int len_g,
+                                                    int n_it, int k, int trash, int lane) {
+        const int l0 = lane % KG;
+        const int n = e_end - e0;  // wave-uniform
+        const auto crs = wave_buffer(col_idx + e0, (uint32_t)n * 4u);
+        const auto vrs = wave_buffer(edge_val + e0, (uint32_t)n * 4u);
+        const auto rrs = wave_buffer(rec, 0xffffffffu);
+        const int lo = (sb_g - e0) * 4;
+        for (int it = 0; it < n_it; ++it) {
+            int c[U];
+            float w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + (it * U + u) * 4, 0, 0);
+                w[u] = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + (it * U + u) * 4, 0, 0));
+            }
+            for (int lb = 0; lb < k; lb += KG) {
+                const int l = lb + l0;
+                const bool lok = l < k;
+                const uint32_t lc = (uint32_t)(lok ? l : k - 1);
+                const uint32_t vo = 4u * lc, so = 4u * (uint32_t)k + 2u * lc;
+                float v[U];
+                int s[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t ro = __umul24((uint32_t)c[u], (uint32_t)RS);
+                    v[u] = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(rrs, (int)(ro + vo), 0, 0));
+                    s[u] = __builtin_amdgcn_raw_buffer_load_b16(rrs, (int)(ro + so), 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const bool live = lok && it * U + u < len_g;
+                    acc_g[live ? s[u] : trash] += w[u] * v[u];
+                }
+            }
+        }
+    }
+
     // acc_g[sel] += val[e] * value over e in [sb, se), sb < se.  acc_g is this
     // lane's group copy.  Padding lanes (l >= k) and edges past se write to the trash
     // column: two lanes of one group must never hit the same live address in one
@@ -284,9 +331,44 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     if (lane == 0) slab_row[item] = cont;
 
     // Rows whose token lies in [d0, d1): this item owns them.
-    for (; r < num_rows; ++r) {
+    while (r < num_rows) {
         const int64_t rb = row_ptr[r];
         if (rb + r >= d1) break;
+        if constexpr (NC > 1 && !WIDE && MAXK_FWD_SHORT > 0) {
+            // Short-row batch: up to NC consecutive rows, each wholly inside the item and at
+            // most MAXK_FWD_SHORT edges long, one per lane group, so a wave keeps NC rows'
+            // loads in flight instead of walking one short row at a time (Flickr: avg
+            // degree 11).  Lane j reads row_ptr[r + j]; the rows' test is wave-uniform.
+            const int rq = r + lane;
+            const int rpj = lane <= NC && rq <= num_rows ? row_ptr[rq] : 0;
+            const int rpn = __shfl_down(rpj, 1);
+            const bool okj = lane < NC && rq < num_rows && (int64_t)rq + rpn < d1 &&
+                             rpn - rpj <= MAXK_FWD_SHORT;
+            const uint64_t bal = __ballot(okj);
+            const int m = __builtin_ctzll(~bal);  // leading rows that qualify
+            if (m >= 2) {
+                const int g = lane / KG;
+                const int sb_g = __shfl(rpj, g < m ? g : 0);
+                const int len_g = g < m ? __shfl(rpn, g) - sb_g : 0;
+                const int e0 = __shfl(rpj, 0), e_end = __shfl(rpj, m);
+                int maxlen = 0;
+                for (int j = 0; j < m; ++j) {
+                    const int lj = __shfl(rpn, j) - __shfl(rpj, j);
+                    maxlen = lj > maxlen ? lj : maxlen;
+                }
+                wave_lds_fence();
+                EdgeWalker<KG, U, WIDE>::run_rows(acc_g, col_idx, edge_val, rec, RS, e0, e_end,
+                                                  sb_g, len_g, (maxlen + U - 1) / U, k, DS - 1,
+                                                  lane);
+                for (int j = 0; j < m; ++j) {
+                    const float div = row_div ? row_div[r + j] : 1.f;
+                    flush_row<1>(acc + j * DS, DS, out + (int64_t)(r + j) * D, D, div,
+                                 row_div != nullptr, lane);
+                }
+                r += m;
+                continue;
+            }
+        }
         int64_t se = (int64_t)row_ptr[r + 1];
         if (d1 - r - 1 < se) se = d1 - r - 1;
         wave_lds_fence();
@@ -295,6 +377,7 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
                                    lane);
         const float div = row_div ? row_div[r] : 1.f;
         flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane);
+        ++r;
     }
 }
 
