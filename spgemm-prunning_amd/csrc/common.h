@@ -66,11 +66,14 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_Q  // pull, k % 4 == 0: quantile-slot selectors + pipelined pull_q_kernel
 #define MAXK_PULL_Q 1
 #endif
-#ifndef MAXK_PULL_H  // pull_q_kernel: parts per tile (destination slots split by rank)
-#define MAXK_PULL_H 2
+#ifndef MAXK_PULL_H  // pull_q_kernel: most parts per tile (destination slots split by rank)
+#define MAXK_PULL_H 16
 #endif
-#ifndef MAXK_PULL_MIN_KP  // pull_q_kernel: fewest slots per destination a part may keep
-#define MAXK_PULL_MIN_KP 16
+#ifndef MAXK_PULL_MIN_KP  // pull_q_kernel: fewest slots per destination a part keeps, k < 32
+#define MAXK_PULL_MIN_KP 8
+#endif
+#ifndef MAXK_PULL_MIN_KP_WIDE  // ... and for k >= 32
+#define MAXK_PULL_MIN_KP_WIDE 16
 #endif
 #ifndef MAXK_PULL_ABL  // tuning only (wrong results): 1 no gathers, 2 no LDS adds, 4 row 0, 8 fixed columns, 16 no entries
 #define MAXK_PULL_ABL 0

@@ -238,16 +238,20 @@ size_t pull_sort_temp_bytes(int64_t num_e, int64_t n_tiles) {
 }  // namespace maxk
 
 // The widest bucket that up to MAXK_PULL_H parts reach (pull_q_kernel, k % (4H) == 0) while
-// a part keeps at least MAXK_PULL_MIN_KP slots: the accumulator holds k/H slots per
-// destination.  Reddit: k = 32 / 64 at H = 2 took 3.93 / 6.28 ms against 4.20 / 8.13 at H = 1;
-// k = 16 at H = 2 (8 slots) 2.72 against 2.62 (profiles/r02/tune/pull_parts.txt).  A part
-// count that does not widen the bucket is not used.  At least 4: the backward copies a
-// bucket's selector rows 16 B at a time (16 | 2^shift * k).
+// a part keeps at least MAXK_PULL_MIN_KP slots (k < 32; MAXK_PULL_MIN_KP_WIDE from k = 32):
+// the accumulator holds k/H slots per destination, so H parts give a bucket H times the
+// destinations and a source row meets H times fewer buckets, for H reads of the entries.
+// Measured (Reddit / proteins, whole backward, profiles/r02/tune/pull_parts_r02.txt):
+// k=16 8 slots 2.43 / 1.23 ms against 16 slots 2.52 / 1.29; k=32 16 slots 3.56 / 1.88 against
+// 8 slots 3.50 / 2.15; k=64 16 slots 5.71 / 3.25 against 32 slots 6.15 / 3.62 and 8 slots
+// 6.15 / 4.07.  A part count that does not widen the bucket is not used.  At least 4: the
+// backward copies a bucket's selector rows 16 B at a time (16 | 2^shift * k).
 extern "C" int maxk_pull_shift(int32_t dim_k) {
     if (dim_k <= 0) return -1;
     int s = maxk_bucket_shift(dim_k);
+    const int kp_min = dim_k >= 32 ? MAXK_PULL_MIN_KP_WIDE : MAXK_PULL_MIN_KP;
     for (int H = 2; MAXK_PULL_Q && H <= MAXK_PULL_H && dim_k % (4 * H) == 0 &&
-                    dim_k / H >= MAXK_PULL_MIN_KP;
+                    dim_k / H >= kp_min;
          H *= 2)
         s = std::max(s, maxk_bucket_shift(dim_k / H));
     const int p = s - MAXK_PULL_SHIFT_DELTA;
