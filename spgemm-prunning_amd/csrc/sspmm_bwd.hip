@@ -787,14 +787,20 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
     // Lane -> (entry g, lane-in-entry q).  The texture path serves a 16-lane quarter in four
     // lane columns {c, c+4, c+8, c+12}, and lanes of one cache line that sit in one quad
     // cost extra cycles (tools/ta_probe.hip, L1-resident: 4 lines per quarter cost 4.2
-    // cycles spread one lane per quad, 8.7 with a quad per line).  An entry's lanes gather
-    // neighbouring sorted columns, often one line, so with LR < 16 a quarter's entries are
-    // interleaved: lane j of the quarter takes entry j % EPQ and lane-in-entry j / EPQ.
+    // cycles spread one lane per quad, 8.7 with a quad per line).  In one instruction the
+    // LR lanes of an entry gather LR consecutive sorted columns, often one line, so they
+    // are spread over the quads and gathered into columns: a column holds four consecutive
+    // lanes-in-entry of one entry (LR >= 4) or all LR lanes of 4/LR neighbouring entries
+    // (LR < 4; neighbours in CSR order share a source row most often).
     constexpr int EPQ = LR < 16 ? 16 / LR : 1;  // entries per 16-lane quarter
-    const int g = MAXK_PULL_TRANSPOSE && LR < 16
-                      ? (lane / 16) * EPQ + (lane % 16) % EPQ
-                      : lane / LR;
-    const int q = MAXK_PULL_TRANSPOSE && LR < 16 ? (lane % 16) / EPQ : lane % LR;
+    const int lc = (lane % 16) % 4, lm = (lane % 16) / 4;  // column, lane's place in it
+    constexpr bool TR = MAXK_PULL_TRANSPOSE && LR <= 16;  // an entry within a quarter
+    const int g = !TR ? lane / LR
+                  : LR >= 4 ? (lane / 16) * EPQ + lc / (LR / 4 > 0 ? LR / 4 : 1)
+                            : (lane / 16) * EPQ + lc * (4 / LR) + lm / LR;
+    const int q = !TR ? lane % LR
+                  : LR >= 4 ? (lc % (LR / 4 > 0 ? LR / 4 : 1)) * 4 + lm
+                            : lm % LR;
     const bool qok = q < kp / 4;
     const int ks = kp + 1;
     const uint32_t Db = (uint32_t)D * 4u;
