@@ -81,6 +81,9 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_TRANSPOSE  // pull_q_kernel: a quarter's entries interleaved across its quads
 #define MAXK_PULL_TRANSPOSE 1
 #endif
+#ifndef MAXK_PULL_VPL8  // pull_q_kernel: values per lane for 8-slot parts (2 or 4)
+#define MAXK_PULL_VPL8 4  // 2 measured slower: Reddit k=16 2.54 vs 2.39 ms
+#endif
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1
 #endif

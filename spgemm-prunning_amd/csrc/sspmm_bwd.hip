@@ -709,7 +709,8 @@ __global__ __launch_bounds__(1024) void pull_tile_kernel(
 __global__ __launch_bounds__(kBlock) void pull_sel_kernel(const uint8_t *__restrict__ sel,
                                                           uint8_t *__restrict__ sel_q,
                                                           uint8_t *__restrict__ lmap,
-                                                          int64_t num_cols, int k, int kp) {
+                                                          int64_t num_cols, int k, int kp,
+                                                          int vpl) {
     __shared__ uint32_t bm[kBlock / 4 * 8];  // 256-bit column set per destination
     __shared__ uint8_t s_out[kBlock], l_out[kBlock];
     const int nd = kBlock / k;  // destinations per block (k % 4 == 0, k <= 256)
@@ -739,8 +740,10 @@ __global__ __launch_bounds__(kBlock) void pull_sel_kernel(const uint8_t *__restr
             }
         }
         // part h = rank / kp (pull_q_kernel's parts), then the quantile slot inside it
-        const int q4 = kp / 4, h = rank / kp, r = rank % kp;
-        const int slot = h * kp + 4 * (r % q4) + r / q4;
+        // lane q of a part holds sorted positions i * (kp / vpl) + q, i < vpl, in slots
+        // vpl * q + i
+        const int ql = kp / vpl, h = rank / kp, r = rank % kp;
+        const int slot = h * kp + vpl * (r % ql) + r / ql;
         s_out[d * k + slot] = (uint8_t)s;
         l_out[d * k + slot] = (uint8_t)l;
     }
@@ -774,7 +777,7 @@ __global__ __launch_bounds__(kBlock) void pull_sel_kernel(const uint8_t *__restr
 //    pulling every slice.
 // One tile's entry loop of pull_q_kernel: adds the tile's n_e entries (ers)
 // into the fp64 accumulator, gathering from the slice's G' rows (grs).
-template <int LR, int U, bool FULLD>
+template <int LR, int U, bool FULLD, int VPL>
 __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_lds,
                                                __amdgpu_buffer_rsrc_t grs,
                                                __amdgpu_buffer_rsrc_t ers, int n_e, int D,
@@ -801,7 +804,7 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
     const int q = !TR ? lane % LR
                   : LR >= 4 ? (lc % (LR / 4 > 0 ? LR / 4 : 1)) * 4 + lm
                             : lm % LR;
-    const bool qok = q < kp / 4;
+    const bool qok = q < kp / VPL;
     const int ks = kp + 1;
     const uint32_t Db = (uint32_t)D * 4u;
     const int stride = 16 * STEP;  // 16 waves
@@ -817,7 +820,7 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
 
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 myA[NL], myB[NL];
-    float vA[U][4], vB[U][4];
+    float vA[U][VPL], vB[U][VPL];
     int dA[U], dB[U];
     float wA[U], wB[U];
     auto load_ent = [&](u32x2(&my)[NL], int n) {
@@ -827,7 +830,7 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
                 ers, (int)((uint32_t)(base + n * stride + m * kWave + lane) * 8u), 0, 0);
     };
     // step n: entries from my (then reloaded for step n + 2), selectors, gathers into v
-    auto issue = [&](u32x2(&my)[NL], float(&v)[U][4], int(&dc)[U], float(&wc)[U], int n) {
+    auto issue = [&](u32x2(&my)[NL], float(&v)[U][VPL], int(&dc)[U], float(&wc)[U], int n) {
         uint32_t ex[U], ey[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -844,8 +847,10 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
         for (int u = 0; u < U; ++u) {
             ok[u] = eb + u * EPI < n_e && qok;
             const int d = ok[u] ? (int)(ex[u] >> 16) : idle;
-            dc[u] = d * ks + 4 * q * ok[u];
-            sv[u] = *reinterpret_cast<const uint32_t *>(sel_lds + d * kp + (ok[u] ? q * 4 : 0));
+            dc[u] = d * ks + VPL * q * ok[u];
+            const uint8_t *sp = sel_lds + d * kp + (ok[u] ? q * VPL : 0);
+            sv[u] = VPL == 4 ? *reinterpret_cast<const uint32_t *>(sp)
+                             : (uint32_t)*reinterpret_cast<const uint16_t *>(sp);
             wc[u] = ok[u] ? __uint_as_float(ey[u]) : 0.0f;
         }
 #pragma unroll
@@ -853,7 +858,7 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
             uint32_t ro = ok[u] ? (ex[u] & 0xffffu) * Db : 0x80000000u;
             if ((MAXK_PULL_ABL & 4) && ok[u]) ro = 0;  // tuning: every entry reads row 0
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < VPL; ++i) {
                 uint32_t c = (sv[u] >> (8 * i)) & 255u;
                 if (MAXK_PULL_ABL & 8) c = 16 * i + 4 * q;  // tuning: 16 contiguous columns
                 uint32_t off = ro + c * 4u;
@@ -867,12 +872,12 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
         }
     };
     float abl_sum = 0.f;
-    auto consume = [&](float(&v)[U][4], int(&dc)[U], float(&wc)[U]) {
+    auto consume = [&](float(&v)[U][VPL], int(&dc)[U], float(&wc)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             double *a = &acc[dc[u]];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < VPL; ++i) {
                 if (MAXK_PULL_ABL & 2)
                     abl_sum += wc[u] * v[u][i] * (float)dc[u];
                 else
@@ -1006,7 +1011,7 @@ __device__ __forceinline__ void pull_flush(const double *acc, float *__restrict_
 //  * tiles in XCD order (MAXK_PULL_XCD): XCD x runs the x-th eighth of the tile sequence
 //    in order, so each XCD's L2 holds the one slice it works on instead of every XCD
 //    pulling every slice.
-template <int LR, int U, bool FULLD>
+template <int LR, int U, bool FULLD, int VPL>
 __global__ __launch_bounds__(1024) void pull_q_kernel(
     const float *__restrict__ Gp, const uint8_t *__restrict__ sel_q,
     const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
@@ -1027,7 +1032,7 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
     const auto grs =
         wave_buffer(Gp + p.r0 * D, (uint32_t)(p.nrows > 0 ? p.nrows : 0) * (uint32_t)D * 4u);
     const auto ers = wave_buffer(ent + p.s0, (uint32_t)(p.s1 - p.s0) * 8u);
-    pull_q_entries<LR, U, FULLD>(acc, sel_lds, grs, ers, p.s1 - p.s0, D, kp, shift);
+    pull_q_entries<LR, U, FULLD, VPL>(acc, sel_lds, grs, ers, p.s1 - p.s0, D, kp, shift);
     __syncthreads();
     pull_flush(acc, tile_out, t, h, k, kp, shift);
 }
@@ -1503,27 +1508,28 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
         uint8_t *sel_q = reinterpret_cast<uint8_t *>(tile_out) + tb;
         uint8_t *lm = sel_q + nsel;
         const int nd = kBlock / k;
+        // values per lane: 2 for 8-slot parts (4 lanes per entry, so a 16-lane quarter holds
+        // 4 entries, not 8), else 4 (one u32 selector word per lane)
+        const int vpl = kp == 8 ? MAXK_PULL_VPL8 : 4;
         hipLaunchKernelGGL(pull_sel_kernel, dim3((unsigned)ceil_div(num_cols, nd)), dim3(kBlock),
-                           0, s, cbsr_idx, sel_q, lm, num_cols, k, kp);
+                           0, s, cbsr_idx, sel_q, lm, num_cols, k, kp, vpl);
         MAXK_LAUNCHED("pull_sel_kernel");
         const int64_t work = (int64_t)tiles * parts;
         const bool fulld = dim_origin == kMaxDim;
         const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);
-        switch (lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
-#define MAXK_CASE(LRV)                                                                        \
-    case LRV * 2 + 1:                                                                         \
-        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, true>), dim3(grid), dim3(1024),   \
-                           lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
-                           (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
-        break;                                                                                \
-    case LRV * 2:                                                                             \
-        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, false>), dim3(grid), dim3(1024),  \
+        switch (vpl == 2 ? (fulld ? -1 : -2) : lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
+#define MAXK_CASE_V(CASE, LRV, FD, VP)                                                        \
+    case CASE:                                                                                \
+        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, FD, VP>), dim3(grid), dim3(1024), \
                            lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
                            (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
         break;
+#define MAXK_CASE(LRV) MAXK_CASE_V(LRV * 2 + 1, LRV, true, 4) MAXK_CASE_V(LRV * 2, LRV, false, 4)
             MAXK_CASE(1) MAXK_CASE(2) MAXK_CASE(4) MAXK_CASE(8) MAXK_CASE(16) MAXK_CASE(32)
             MAXK_CASE(64)
+            MAXK_CASE_V(-1, 4, true, 2) MAXK_CASE_V(-2, 4, false, 2)
 #undef MAXK_CASE
+#undef MAXK_CASE_V
             default:
                 set_error("unsupported lane group");
                 return MAXK_ERR_INVALID;

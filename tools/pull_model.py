@@ -183,3 +183,39 @@ if os.environ.get("PARTS"):
                 l2 += L2_LINES[0]
             print(f"  H={H} LR={LR:2d} VPL={k // H // LR:2d}: {cyc / n_ent:6.2f} TA cyc  "
                   f"{l2 / n_ent:5.2f} L2 lines per entry")
+
+
+def order_hybrid(r, c, epq, T):
+    """Entries of a tile reordered: rows whose run is >= T first, each run padded to a
+    multiple of epq (dummy entries -1), then the shorter runs packed in CSR order."""
+    u, start, cnt = np.unique(r, return_index=True, return_counts=True)
+    lr, lc, sr, sc = [], [], [], []
+    for s0, n0 in zip(start, cnt):
+        if n0 >= T:
+            p = (-n0) % epq
+            lr.append(np.concatenate([r[s0:s0 + n0], np.full(p, -1)]))
+            lc.append(np.concatenate([c[s0:s0 + n0], np.zeros(p, np.int64)]))
+        else:
+            sr.append(r[s0:s0 + n0])
+            sc.append(c[s0:s0 + n0])
+    rr = np.concatenate(lr + sr) if lr or sr else r
+    cc = np.concatenate(lc + sc) if lc or sc else c
+    return rr, cc
+
+
+if os.environ.get("HYBRID"):
+    H = int(os.environ.get("H", "2"))
+    LR = k // H // 4
+    epq = 16 // LR
+    print(f"hybrid order, H={H} parts, LR={LR} (tag model: max(4, lines) per quarter)")
+    for T in (0, 4, 8, 16, 32):
+        cyc = l2 = pads = 0
+        for t in ts:
+            r, c = tile(int(t))
+            rr, cc = (r, c) if T == 0 else order_hybrid(r, c, epq, T)
+            pads += (rr < 0).sum()
+            L2_LINES[0] = 0
+            cyc += layout_parts(rr, np.where(rr < 0, 0, cc), LR, H)
+            l2 += L2_LINES[0]
+        print(f"  T={T:2d}: {cyc / n_ent:6.2f} TA cyc/entry  {l2 / n_ent:5.2f} L2 lines/entry (no L1)  "
+              f"padding {pads / n_ent:.1%}")
