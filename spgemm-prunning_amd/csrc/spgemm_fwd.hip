@@ -330,7 +330,11 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     }
     if (lane == 0) slab_row[item] = cont;
 
-    // Rows whose token lies in [d0, d1): this item owns them.
+    // Rows whose token lies in [d0, d1): this item owns them.  row_ptr of 64 consecutive rows
+    // sits one per lane (window from row wb), for the short-row test below.
+    int wb = r, rpw = 0;
+    if constexpr (NC > 1 && !WIDE && MAXK_FWD_SHORT > 0)
+        rpw = row_ptr[r + lane <= num_rows ? r + lane : num_rows];
     while (r < num_rows) {
         const int64_t rb = row_ptr[r];
         if (rb + r >= d1) break;
@@ -338,9 +342,14 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
             // Short-row batch: up to NC consecutive rows, each wholly inside the item and at
             // most MAXK_FWD_SHORT edges long, one per lane group, so a wave keeps NC rows'
             // loads in flight instead of walking one short row at a time (Flickr: avg
-            // degree 11).  Lane j reads row_ptr[r + j]; the rows' test is wave-uniform.
+            // degree 11).  The test reads the row_ptr window (no load per row): long rows
+            // pay only a few shuffles for it.
+            if (r + NC >= wb + kWave) {  // slide the window
+                wb = r;
+                rpw = row_ptr[r + lane <= num_rows ? r + lane : num_rows];
+            }
             const int rq = r + lane;
-            const int rpj = lane <= NC && rq <= num_rows ? row_ptr[rq] : 0;
+            const int rpj = __shfl(rpw, (r - wb + lane) & (kWave - 1));
             const int rpn = __shfl_down(rpj, 1);
             const bool okj = lane < NC && rq < num_rows && (int64_t)rq + rpn < d1 &&
                              rpn - rpj <= MAXK_FWD_SHORT;
