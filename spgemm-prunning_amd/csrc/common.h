@@ -87,6 +87,9 @@ constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1
 #endif
+#ifndef MAXK_BWD_ABL  // tuning only (wrong results): 1 phase-1 selectors from a 4096-row table, 2 no T stores but the last
+#define MAXK_BWD_ABL 0
+#endif
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif

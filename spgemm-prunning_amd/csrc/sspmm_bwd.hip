@@ -69,6 +69,7 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
     const uint32_t qst = q < k4 ? 16u * q : 0x80000000u;  // store offset term; past the end if idle
     const uint32_t kb = 4u * (uint32_t)k;                    // T row bytes
     auto sel_off = [&](int c) -> int {
+        if (MAXK_BWD_ABL & 1) c &= 4095;  // tuning: selectors from a 4096-row table
         return WIDE ? (int)((uint32_t)c * (uint32_t)k + qsel)
                     : (int)(__umul24((uint32_t)c, (uint32_t)k) + qsel);
     };
@@ -102,7 +103,7 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
 #pragma unroll
         for (int u = 0; u < U; ++u)
             sv[u] = __builtin_amdgcn_raw_buffer_load_b32(srs, sel_off(c[u]), 0, 0);
-        if (pending) {
+        if (pending && !(MAXK_BWD_ABL & 2)) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0,
@@ -126,8 +127,10 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
         }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+        if (MAXK_BWD_ABL & 2) xp[u].x += xp[u].y;  // tuning: keep the products live
         __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0, MAXK_T_AUX);
+    }
 }
 
 // Walk edges [sb, se) (sb < se) of one staged row.  All loads are
