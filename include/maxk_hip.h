@@ -159,8 +159,12 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
  * repeatability: maxk_sspmm_backward_csc).  For dim_k % 4 == 0 each destination's selectors
  * are first re-ordered by column (quantile slots, sspmm_bwd.hip pull_sel_kernel) so one
  * gather instruction touches fewer lines of a row; the sums return to CBSR order at the
- * end.  A selector >= dim_origin contributes 0.  Needs dim_k % 4 == 0 or dim_k <= 64,
- * dim_origin % 4 == 0, bucket_shift in [4, min(15, maxk_bucket_shift(dim_k))], the pull
+ * end.  With dim_k % 4 == 0 a tile's destination slots may be split by sorted rank into
+ * parts of kp = dim_k / H slots, one workgroup each, so a bucket holds H times the
+ * destinations (kp >= 8 below dim_k = 32, >= 16 from 32; maxk_pull_shift(dim_k) gives the
+ * matching shift).  A selector >= dim_origin contributes 0.  Needs dim_k % 4 == 0 or
+ * dim_k <= 64, dim_origin % 4 == 0, bucket_shift in [4, min(15, max(maxk_bucket_shift(dim_k),
+ * maxk_pull_shift(dim_k)))] (above maxk_bucket_shift(dim_k) only with dim_k % 4 == 0), the pull
  * plan of the graph built with the same shift, slices and edge_val (maxk_pull_plan), and a
  * workspace of maxk_sspmm_backward_pull_workspace_size(...) bytes (G / row_div, slices x
  * num_cols x k floats of tile partials, and 2 x num_cols x k bytes of slot-ordered

@@ -219,3 +219,36 @@ if os.environ.get("HYBRID"):
             l2 += L2_LINES[0]
         print(f"  T={T:2d}: {cyc / n_ent:6.2f} TA cyc/entry  {l2 / n_ent:5.2f} L2 lines/entry (no L1)  "
               f"padding {pads / n_ent:.1%}")
+
+if os.environ.get("DEGSORT"):
+    # relabel vertices by descending degree (rows and columns alike) and redo the floor
+    deg = np.diff(rp)
+    order = np.argsort(-deg, kind="stable")
+    newid = np.empty(V, np.int64)
+    newid[order] = np.arange(V)
+    r2 = newid[rows]
+    c2 = newid[col]
+    o = np.lexsort((c2, r2))
+    rows, col = r2[o], c2[o].astype(np.int32)
+    rp = np.zeros(V + 1, np.int64)
+    np.cumsum(np.bincount(rows, minlength=V), out=rp[1:])
+    sel = sel[order]  # selectors follow their vertex
+    lm = 0
+    n2 = 0
+    cyc = 0
+    for t in ts:
+        r, c = tile(int(t))
+        n2 += len(r)
+        if len(r):
+            lm += len(np.unique(r[:, None] * 8 + sel[c] // 32))
+            cyc += layout_A(r, c, 4)
+    print(f"degree-sorted labels: {n2} entries in the same tiles; floor {lm / max(n2,1):5.2f} lines/entry, "
+          f"TA model LR=4 {cyc / max(n2,1):5.2f} cyc/entry")
+    # all tiles weighted: sample more tiles uniformly over entries
+    tot_l = tot_e = 0
+    for t in rng.choice(a.slices * nb, size=64, replace=False):
+        r, c = tile(int(t))
+        if len(r):
+            tot_l += len(np.unique(r[:, None] * 8 + sel[c] // 32))
+            tot_e += len(r)
+    print(f"  64 random tiles: floor {tot_l / tot_e:5.2f} lines/entry over {tot_e} entries")
