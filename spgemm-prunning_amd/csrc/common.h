@@ -244,27 +244,65 @@ __global__ __launch_bounds__(kBlock) void slab_fixup_kernel(const float *__restr
                                                             int n_items) {
     const int item = (int)((blockIdx.x * (int64_t)kBlock + threadIdx.x) / 16);
     const int g = threadIdx.x % 16;
+    const int grp = (threadIdx.x % kWave) / 16;  // this item's lane group in the wave
     if (item >= n_items) return;
     const int row = slab_row[item];
     if (row < 0 || (item > 0 && slab_row[item - 1] == row)) return;
+    // n = this row's slabs (consecutive items), found 16 items per step by the group's lanes:
+    // a hub row cut into many items (a vertex-range shard's small chunks: Reddit's max-degree
+    // row spans ~80 items of 256 tokens) would otherwise cost one dependent load per slab.
+    int n = 1;
+    for (int base = item + 1;; base += 16) {
+        const int i = base + g;
+        const bool same = i < n_items && slab_row[i] == row;
+        const uint32_t mine = (uint32_t)(__ballot(same) >> (16 * grp)) & 0xffffu;
+        const int run = __builtin_ctz(~mine | 0x10000u);
+        n += run;
+        if (run < 16) break;
+    }
     float *o = out + (int64_t)row * width;
-    if ((width & 3) == 0) {
-        for (int j = g * 4; j < width; j += 64) {
-            float4 a = *reinterpret_cast<const float4 *>(o + j);
-            for (int i = item; i < n_items && slab_row[i] == row; ++i) {
-                const float4 b = *reinterpret_cast<const float4 *>(slab + (int64_t)i * width + j);
-                a.x += b.x;
-                a.y += b.y;
-                a.z += b.z;
-                a.w += b.w;
+    const float *sl = slab + (int64_t)item * width;
+    if ((width & 3) == 0 && width <= 256) {
+        // up to 4 float4 columns per lane; slabs added in item order, 4 x 4 loads in flight
+        constexpr int SU = 4;
+        float4 a[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int j = g * 4 + 64 * c;
+            a[c] = j < width ? *reinterpret_cast<const float4 *>(o + j) : make_float4(0, 0, 0, 0);
+        }
+        for (int i0 = 0; i0 < n; i0 += SU) {
+            float4 b[SU][4];
+#pragma unroll
+            for (int u = 0; u < SU; ++u)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int j = g * 4 + 64 * c;
+                    const int i = i0 + u < n ? i0 + u : n - 1;  // clamped: loaded, not added
+                    b[u][c] = j < width ? *reinterpret_cast<const float4 *>(sl + (int64_t)i * width + j)
+                                        : make_float4(0, 0, 0, 0);
+                }
+#pragma unroll
+            for (int u = 0; u < SU; ++u) {
+                if (i0 + u >= n) break;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    a[c].x += b[u][c].x;
+                    a[c].y += b[u][c].y;
+                    a[c].z += b[u][c].z;
+                    a[c].w += b[u][c].w;
+                }
             }
-            *reinterpret_cast<float4 *>(o + j) = a;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int j = g * 4 + 64 * c;
+            if (j < width) *reinterpret_cast<float4 *>(o + j) = a[c];
         }
     } else {
         for (int j = g; j < width; j += 16) {
             float a = o[j];
-            for (int i = item; i < n_items && slab_row[i] == row; ++i)
-                a += slab[(int64_t)i * width + j];
+            for (int i = 0; i < n; ++i) a += sl[(int64_t)i * width + j];
             o[j] = a;
         }
     }
