@@ -758,26 +758,6 @@ __global__ __launch_bounds__(kBlock) void pull_sel_kernel(const uint8_t *__restr
     }
 }
 
-// Parts: with H = k / kp parts, destination c's slots split by sorted position into H
-// groups of kp (part h: the h-th kp smallest selectors), and one workgroup sums one part of
-// one tile: the accumulator holds kp slots per destination, so a bucket holds H times the
-// destinations and a source row meets ~H times fewer buckets; each part's gathers cover
-// only its share of a row's columns (the h-th kp order statistics of every entry).  The
-// tile's entries are read H times.  Model of the Reddit stream (k = 16): L2 lines per entry
-// 3.2 -> 2.3 at H = 2.
-// One 1024-thread workgroup per (tile, part), as pull_tile_kernel (fp64 LDS accumulator of
-// the bucket, its slot-ordered selector rows copied next to it), with:
-//  * quantile slots (above): lane q's u32 selector word holds its four instructions'
-//    columns;
-//  * a two-step software pipeline: step n's gathers are issued before step n-1's adds, and
-//    the entries two steps ahead, so a wave keeps 2 x 4U gathers in flight and never waits
-//    on loads it has just issued (the one-step loop waited for every load at its head);
-//  * the G' gathers through a wave-uniform buffer descriptor over the slice's rows with
-//    32-bit offsets (no 64-bit address math per value); a selector >= D (possible only
-//    when D < 256, !FULLD) gets an offset past the descriptor, and the hardware returns 0;
-//  * tiles in XCD order (MAXK_PULL_XCD): XCD x runs the x-th eighth of the tile sequence
-//    in order, so each XCD's L2 holds the one slice it works on instead of every XCD
-//    pulling every slice.
 // One tile's entry loop of pull_q_kernel: adds the tile's n_e entries (ers)
 // into the fp64 accumulator, gathering from the slice's G' rows (grs).
 template <int LR, int U, bool FULLD, int VPL>
@@ -999,12 +979,11 @@ __device__ __forceinline__ void pull_flush(const double *acc, float *__restrict_
 // one tile: the accumulator holds kp slots per destination, so a bucket holds H times the
 // destinations and a source row meets ~H times fewer buckets; each part's gathers cover
 // only its share of a row's columns (the h-th kp order statistics of every entry).  The
-// tile's entries are read H times.  Model of the Reddit stream (k = 16): L2 lines per entry
-// 3.2 -> 2.3 at H = 2.
+// tile's entries are read H times (kp: maxk_pull_shift, transpose.hip).
 // One 1024-thread workgroup per (tile, part), as pull_tile_kernel (fp64 LDS accumulator of
 // the bucket, its slot-ordered selector rows copied next to it), with:
-//  * quantile slots (above): lane q's u32 selector word holds its four instructions'
-//    columns;
+//  * quantile slots (pull_sel_kernel): lane q's u32 selector word holds its four
+//    instructions' columns;
 //  * a two-step software pipeline: step n's gathers are issued before step n-1's adds, and
 //    the entries two steps ahead, so a wave keeps 2 x 4U gathers in flight and never waits
 //    on loads it has just issued (the one-step loop waited for every load at its head);
