@@ -51,6 +51,11 @@ constexpr int kBucketAccDoubles = 18432;
 #define MAXK_PULL_SHIFT_DELTA 0
 #endif
 constexpr size_t kPullLdsBytes = 160 * 1024;  // LDS of one workgroup on gfx950
+// pull_q_kernel accumulator row stride in doubles: kp + 1 (the pad spreads a wave's
+// destinations over the LDS banks) when the padded bucket fits, else kp
+__host__ __device__ inline int pull_ks(int kp, int shift) {
+    return ((((size_t)(kp + 1) * 8 + kp) << shift) <= kPullLdsBytes) ? kp + 1 : kp;
+}
 #ifndef MAXK_PULL_SHFL  // pull: the step's entries by one load + lane shuffles
 #define MAXK_PULL_SHFL 1
 #endif

@@ -788,7 +788,7 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
                   : LR >= 4 ? (lc % (LR / 4 > 0 ? LR / 4 : 1)) * 4 + lm
                             : lm % LR;
     const bool qok = q < kp / VPL;
-    const int ks = kp + 1;
+    const int ks = pull_ks(kp, shift);
     const uint32_t Db = (uint32_t)D * 4u;
     const int stride = 16 * STEP;  // 16 waves
     const int base = w * STEP;     // entry offsets relative to the tile's first entry
@@ -963,7 +963,7 @@ __device__ __forceinline__ void pull_sel_store(uint8_t *sel_lds, const PullSel &
 // tile_out[t] is [2^shift, k] in slot order; part h fills slots [h * kp, (h + 1) * kp).
 __device__ __forceinline__ void pull_flush(const double *acc, float *__restrict__ tile_out, int t,
                                            int h, int k, int kp, int shift) {
-    const int ks = kp + 1;
+    const int ks = pull_ks(kp, shift);
     float *o = tile_out + (size_t)t * ((size_t)k << shift) + h * kp;
     const int w4 = kp / 4;
     for (int i4 = threadIdx.x; i4 < (kp << shift) / 4; i4 += 1024) {
@@ -999,9 +999,9 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
     const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
     float *__restrict__ tile_out, int64_t num_cols, int n_buckets, int n_tiles,
     int rows_per_slice, int64_t num_rows, int D, int k, int kp, int shift) {
-    extern __shared__ double acc[];  // [(kp + 1) << shift], then [kp << shift] selector bytes
+    extern __shared__ double acc[];  // [ks << shift], then [kp << shift] selector bytes
     const int tid = threadIdx.x;
-    const int ks = kp + 1;
+    const int ks = pull_ks(kp, shift);
     const int H = k / kp;
     const int tp = MAXK_PULL_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
     if (tp >= n_tiles * H) return;  // the XCD grid's padding
@@ -1405,7 +1405,7 @@ int pull_parts(int k, int shift) {
     for (int H = 1; H <= k / 4; H *= 2) {
         if (k % (4 * H)) break;
         const int kp = k / H;
-        if ((((size_t)(kp + 1) * 8 + kp) << shift) <= kPullLdsBytes) return H;
+        if ((((size_t)kp * 8 + kp) << shift) <= kPullLdsBytes) return H;  // unpadded fits
     }
     return 0;
 }
@@ -1484,7 +1484,7 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     const uint8_t *lmap = nullptr;
     if (parts > 0) {  // quantile-slot form (pull_q_kernel), `parts` workgroups per tile
         const int kp = k / parts;
-        const size_t lds_q = ((size_t)(kp + 1) * 8 + kp) << bucket_shift;
+        const size_t lds_q = ((size_t)pull_ks(kp, bucket_shift) * 8 + kp) << bucket_shift;
         const size_t tb = (size_t)slices * nb * ((size_t)k << bucket_shift) * sizeof(float);
         const size_t nsel = ((size_t)num_cols * k + 255) & ~(size_t)255;
         uint8_t *sel_q = reinterpret_cast<uint8_t *>(tile_out) + tb;

@@ -252,8 +252,13 @@ extern "C" int maxk_pull_shift(int32_t dim_k) {
     const int kp_min = dim_k >= 32 ? MAXK_PULL_MIN_KP_WIDE : MAXK_PULL_MIN_KP;
     for (int H = 2; MAXK_PULL_Q && H <= MAXK_PULL_H && dim_k % (4 * H) == 0 &&
                     dim_k / H >= kp_min;
-         H *= 2)
-        s = std::max(s, maxk_bucket_shift(dim_k / H));
+         H *= 2) {
+        // the widest bucket whose kp-slot rows (unpadded, maxk::pull_ks) and selectors fit
+        const int kp = dim_k / H;
+        int sh = 0;
+        while (sh < 15 && (((size_t)kp * 8 + kp) << (sh + 1)) <= maxk::kPullLdsBytes) ++sh;
+        s = std::max(s, sh);
+    }
     const int p = s - MAXK_PULL_SHIFT_DELTA;
     return p < 4 ? 4 : (p > 15 ? 15 : p);
 }
