@@ -263,12 +263,25 @@ extern "C" int maxk_pull_shift(int32_t dim_k) {
     return p < 4 ? 4 : (p > 15 ? 15 : p);
 }
 
-// ~3.5 MiB of G rows per slice up to k = 16, k/16 times that above: the S tile partials
-// (S x num_cols x k floats, written and read once) grow with k, the gather locality does not
-// (Reddit: S = 66 / 33 / 16 best at k = 16 / 32 / 64, profiles/r01/tune/pull_slices_k.txt).
+// Parts per tile the pull backward uses at width k (the largest H of maxk_pull_shift's rule:
+// k % (4H) == 0 and k/H slots at least MAXK_PULL_MIN_KP, or _WIDE from k = 32).
+static int pull_parts_of(int32_t dim_k) {
+    int H = 1;
+    const int kp_min = dim_k >= 32 ? MAXK_PULL_MIN_KP_WIDE : MAXK_PULL_MIN_KP;
+    while (MAXK_PULL_Q && 2 * H <= MAXK_PULL_H && dim_k % (8 * H) == 0 && dim_k / (2 * H) >= kp_min)
+        H *= 2;
+    return H;
+}
+
+// ~3.5 MiB of G rows per slice and part: a part gathers only its share of a row's columns
+// (its rank range of the sorted selectors), so an XCD's L2 holds H times the rows of G for
+// it.  The S tile partials (S x num_cols x k floats, written and read once) fall as the
+// slices grow.  Reddit (whole backward, profiles/r02/tune/pull_slices_r02.txt): k = 16
+// (2 parts) best at S = 30-34 (2.23 ms against 2.42 at S = 66), k = 8 (1 part) flat over
+// 40-66, k = 32 (2 parts) at 33, k = 64 (4 parts) at 17.
 extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
-    const int64_t per = maxk::kPullSliceBytes * (dim_k > 16 ? dim_k / 16 : 1);
+    const int64_t per = maxk::kPullSliceBytes * (dim_k % 4 == 0 ? pull_parts_of(dim_k) : 1);
     int64_t s = (num_rows * dim_origin * 4 + per - 1) / per;
     const int64_t lo = (num_rows + 65535) / 65536;  // rows within a slice fit 16 bits
     s = s < lo ? lo : s;
