@@ -187,7 +187,8 @@ int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
  * (column - first column of its bucket) << 16, bits of edge_val}; bucket_shift in [4, 15]
  * (the backward's 16-B selector copies need 16 | 2^shift * k).  maxk_pull_shift(k) is the
  * bucket shift to use (at least 4); maxk_pull_slices(num_rows, dim_origin, dim_k) the default
- * slice count (about 3.5 MiB of G rows per slice, at least num_rows/65536, 1..256). */
+ * slice count (about 3.5 MiB of G rows per slice and rank part of k -- at most 3 parts' worth
+ * -- at least num_rows/65536, 1..256). */
 int maxk_pull_shift(int32_t dim_k);
 int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,

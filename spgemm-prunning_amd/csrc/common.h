@@ -86,8 +86,11 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_TRANSPOSE  // pull_q_kernel: a quarter's entries interleaved across its quads
 #define MAXK_PULL_TRANSPOSE 1
 #endif
-#ifndef MAXK_PULL_VPL8  // pull_q_kernel: values per lane for 8-slot parts (2 or 4)
-#define MAXK_PULL_VPL8 4  // 2 measured slower: Reddit k=16 2.54 vs 2.39 ms
+// pull_q_kernel: values per lane for 8-slot parts (2, 4 or 8; 0: 8 when k = 8, else 4).
+// Reddit (profiles/r02/tune/pull_vpl.txt): k = 16 VPL 2 / 4 / 8 = 2.54 / 2.39 / 2.41 ms
+// (2.23 / 2.25 at S = 33); k = 8 VPL 4 / 8 = 1.54 / 1.50 ms
+#ifndef MAXK_PULL_VPL8
+#define MAXK_PULL_VPL8 0
 #endif
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1

@@ -823,7 +823,7 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
             ey[u] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)my[m][1]);
         }
         load_ent(my, n + 2);
-        uint32_t sv[U];
+        uint64_t sv[U];
         bool ok[U];
         const int eb = base + n * stride + g;  // this lane group's entry of instruction 0
 #pragma unroll
@@ -832,8 +832,12 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
             const int d = ok[u] ? (int)(ex[u] >> 16) : idle;
             dc[u] = d * ks + VPL * q * ok[u];
             const uint8_t *sp = sel_lds + d * kp + (ok[u] ? q * VPL : 0);
-            sv[u] = VPL == 4 ? *reinterpret_cast<const uint32_t *>(sp)
-                             : (uint32_t)*reinterpret_cast<const uint16_t *>(sp);
+            if constexpr (VPL == 8)
+                sv[u] = *reinterpret_cast<const uint64_t *>(sp);
+            else if constexpr (VPL == 4)
+                sv[u] = *reinterpret_cast<const uint32_t *>(sp);
+            else
+                sv[u] = *reinterpret_cast<const uint16_t *>(sp);
             wc[u] = ok[u] ? __uint_as_float(ey[u]) : 0.0f;
         }
 #pragma unroll
@@ -842,7 +846,8 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
             if ((MAXK_PULL_ABL & 4) && ok[u]) ro = 0;  // tuning: every entry reads row 0
 #pragma unroll
             for (int i = 0; i < VPL; ++i) {
-                uint32_t c = (sv[u] >> (8 * i)) & 255u;
+                uint32_t c = VPL == 8 ? (uint32_t)(sv[u] >> (8 * i)) & 255u
+                                      : ((uint32_t)sv[u] >> (8 * i)) & 255u;
                 if (MAXK_PULL_ABL & 8) c = 16 * i + 4 * q;  // tuning: 16 contiguous columns
                 uint32_t off = ro + c * 4u;
                 if (!FULLD) off = c < (uint32_t)D ? off : 0x80000000u;  // past the buffer: 0
@@ -1490,16 +1495,18 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
         uint8_t *sel_q = reinterpret_cast<uint8_t *>(tile_out) + tb;
         uint8_t *lm = sel_q + nsel;
         const int nd = kBlock / k;
-        // values per lane: 2 for 8-slot parts (4 lanes per entry, so a 16-lane quarter holds
-        // 4 entries, not 8), else 4 (one u32 selector word per lane)
-        const int vpl = kp == 8 ? MAXK_PULL_VPL8 : 4;
+        // values per lane: 4 (one u32 selector word per lane; 2 lanes per entry for 8-slot
+        // parts), 8 for k = 8 (one lane per entry, one u64 selector word; MAXK_PULL_VPL8)
+        const int vpl = kp != 8 ? 4 : MAXK_PULL_VPL8 ? MAXK_PULL_VPL8 : parts == 1 ? 8 : 4;
         hipLaunchKernelGGL(pull_sel_kernel, dim3((unsigned)ceil_div(num_cols, nd)), dim3(kBlock),
                            0, s, cbsr_idx, sel_q, lm, num_cols, k, kp, vpl);
         MAXK_LAUNCHED("pull_sel_kernel");
         const int64_t work = (int64_t)tiles * parts;
         const bool fulld = dim_origin == kMaxDim;
         const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);
-        switch (vpl == 2 ? (fulld ? -1 : -2) : lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
+        switch (vpl == 2   ? (fulld ? -1 : -2)
+                : vpl == 8 ? (fulld ? -3 : -4)
+                           : lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
 #define MAXK_CASE_V(CASE, LRV, FD, VP)                                                        \
     case CASE:                                                                                \
         hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, FD, VP>), dim3(grid), dim3(1024), \
@@ -1510,6 +1517,7 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
             MAXK_CASE(1) MAXK_CASE(2) MAXK_CASE(4) MAXK_CASE(8) MAXK_CASE(16) MAXK_CASE(32)
             MAXK_CASE(64)
             MAXK_CASE_V(-1, 4, true, 2) MAXK_CASE_V(-2, 4, false, 2)
+            MAXK_CASE_V(-3, 1, true, 8) MAXK_CASE_V(-4, 1, false, 8)
 #undef MAXK_CASE
 #undef MAXK_CASE_V
             default:

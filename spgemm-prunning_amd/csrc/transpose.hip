@@ -278,10 +278,13 @@ static int pull_parts_of(int32_t dim_k) {
 // it.  The S tile partials (S x num_cols x k floats, written and read once) fall as the
 // slices grow.  Reddit (whole backward, profiles/r02/tune/pull_slices_r02.txt): k = 16
 // (2 parts) best at S = 30-34 (2.23 ms against 2.42 at S = 66), k = 8 (1 part) flat over
-// 40-66, k = 32 (2 parts) at 33, k = 64 (4 parts) at 17.
+// 40-66, k = 32 (2 parts) at 33.  Past 3 parts the gain stops: k = 64 (4 parts) runs 5.32 ms
+// at S = 20-22 against 5.74 at 17 (profiles/r02/tune/pull_slices_k64.txt), so the factor is
+// capped at 3 (proteins k = 64 is flat over S = 8-12).
 extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
-    const int64_t per = maxk::kPullSliceBytes * (dim_k % 4 == 0 ? pull_parts_of(dim_k) : 1);
+    const int parts = dim_k % 4 == 0 ? pull_parts_of(dim_k) : 1;
+    const int64_t per = maxk::kPullSliceBytes * (parts < 3 ? parts : 3);
     int64_t s = (num_rows * dim_origin * 4 + per - 1) / per;
     const int64_t lo = (num_rows + 65535) / 65536;  // rows within a slice fit 16 bits
     s = s < lo ? lo : s;

@@ -316,7 +316,7 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
               k: int, dim: int = 256, slices: Optional[int] = None, cache: bool = True):
     """(tile_ptr int32 [S*nb+1], ent int32 [E, 2], shift, S) of a CSR graph and its edge
     values for the pull backward at width k: rows cut into S slices (default
-    maxk_pull_slices: ~3.5 MiB of G rows each, k/16 times that above k=16), columns into
+    maxk_pull_slices: ~3.5 MiB of G rows per slice and rank part, at most 3 parts), columns into
     buckets of 2^shift; per tile
     (slice, bucket) the edges in CSR order, each {row in its slice | column in its bucket
     << 16, weight bits}.  Built on the GPU (one stable radix sort); cached per

@@ -179,18 +179,19 @@ def test_bucket_shift_rule():
 
 
 def test_pull_slice_rule():
-    """~3.5 MiB of G rows per slice, clamped to [1, 256]; the pull workspace is G / row_div
-    plus one fp32 partial [num_cols padded to buckets, k] per slice."""
+    """~3.5 MiB of G rows per slice and rank part (at most 3 parts' worth), clamped to
+    [1, 256]; the pull workspace is G / row_div plus one fp32 partial [num_cols padded to
+    buckets, k] per slice."""
     from maxk_cuda_kernels import _capi
     L = _capi.load()
-    assert L.maxk_pull_slices(232965, 256, 16) == 66  # Reddit: 238.6 MB of G rows
-    assert L.maxk_pull_slices(232965, 256, 8) == 66
-    assert L.maxk_pull_slices(232965, 256, 32) == 33  # k/16 x the bytes per slice above k=16
-    assert L.maxk_pull_slices(232965, 256, 64) == 17
-    assert L.maxk_pull_slices(29121, 256, 16) == 9    # one of 8 row shards
+    assert L.maxk_pull_slices(232965, 256, 16) == 33  # Reddit: 238.6 MB of G rows, 2 parts
+    assert L.maxk_pull_slices(232965, 256, 8) == 66   # 1 part
+    assert L.maxk_pull_slices(232965, 256, 32) == 33  # 2 parts
+    assert L.maxk_pull_slices(232965, 256, 64) == 22  # 4 parts, factor capped at 3
+    assert L.maxk_pull_slices(29121, 256, 16) == 5    # one of 8 row shards
     assert L.maxk_pull_slices(1, 256, 16) == 1 and L.maxk_pull_slices(0, 256, 16) == 1
     assert L.maxk_pull_slices(100_000_000, 256, 16) == 256
-    assert L.maxk_pull_slices(2_449_029, 256, 64) == 171
+    assert L.maxk_pull_slices(2_449_029, 256, 64) == 228
     assert L.maxk_pull_slices(4_000_000, 16, 64) == 62  # rows in a slice stay <= 65536
     gp = (232965 * 256 * 4 + 255) // 256 * 256
     selq = 2 * ((232965 * 16 + 255) // 256 * 256)  # slot-ordered selectors + their l map
