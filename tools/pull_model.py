@@ -252,3 +252,26 @@ if os.environ.get("DEGSORT"):
             tot_l += len(np.unique(r[:, None] * 8 + sel[c] // 32))
             tot_e += len(r)
     print(f"  64 random tiles: floor {tot_l / tot_e:5.2f} lines/entry over {tot_e} entries")
+
+if os.environ.get("ROWSTAGE"):
+    # rows whose run in a tile is >= T entries: one coalesced 1-KB load of the row per
+    # (row, tile, part) = 4 quarters x max(4, 2 lines) = 16 cycles, the values then picked
+    # from registers; shorter runs as now (layout_parts, CSR order)
+    H = int(os.environ.get("H", "2"))
+    LR = k // H // 4
+    print(f"row-staged hybrid, H={H} parts, LR={LR}: TA cycles per entry")
+    for T in (0, 4, 8, 16, 32, 64):
+        cyc = ent_long = 0
+        for t in ts:
+            r, c = tile(int(t))
+            u, start, cnt = np.unique(r, return_index=True, return_counts=True)
+            longm = np.repeat(cnt >= T if T else np.zeros_like(cnt, bool), cnt)
+            order = np.argsort(r, kind="stable")  # r already sorted (CSR order)
+            ent_long += longm.sum()
+            lg = cnt[cnt >= T] if T else cnt[:0]
+            # per part: the row (16) and its entries, one b64 per lane per 64 (16 each)
+            cyc += H * int((16 + 16 * -(-lg // 64)).sum())
+            rs, cs = r[~longm], c[~longm]
+            if len(rs):
+                cyc += layout_parts(rs, cs, LR, H)
+        print(f"  T={T:3d}: {cyc / n_ent:6.2f} TA cyc/entry (all parts)  long-run entries {ent_long / n_ent:.1%}")
