@@ -95,7 +95,8 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1
 #endif
-#ifndef MAXK_BWD_ABL  // tuning only (wrong results): 1 phase-1 selectors from a 4096-row table, 2 no T stores but the last
+#ifndef MAXK_BWD_ABL  // tuning only (wrong results): 1 phase-1 selectors from a 4096-row table, 2 no T stores but the last,
+                      // 4 csc phase 2 reads T rows in order (no eid), 8 phase-1 T rows stored at hashed rows
 #define MAXK_BWD_ABL 0
 #endif
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1

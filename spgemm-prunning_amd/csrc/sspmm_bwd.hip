@@ -103,7 +103,16 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
 #pragma unroll
         for (int u = 0; u < U; ++u)
             sv[u] = __builtin_amdgcn_raw_buffer_load_b32(srs, sel_off(c[u]), 0, 0);
-        if (pending && !(MAXK_BWD_ABL & 2)) {
+        if (pending && (MAXK_BWD_ABL & 8)) {  // tuning: scattered whole-row stores
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t er = (sto - qst) / kb + u * G;  // row within the segment
+                if (q < k4 && er < (uint32_t)n) {
+                    const uint32_t h = ((uint32_t)sb + er) * 2654435761u & ((1u << 26) - 1u);
+                    *reinterpret_cast<u32x4 *>(T + (size_t)h * k + 4 * q) = xp[u];
+                }
+            }
+        } else if (pending && !(MAXK_BWD_ABL & 2)) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0,
@@ -129,6 +138,14 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         if (MAXK_BWD_ABL & 2) xp[u].x += xp[u].y;  // tuning: keep the products live
+        if (MAXK_BWD_ABL & 8) {
+            const uint32_t er = (sto - qst) / kb + u * G;
+            if (q < k4 && er < (uint32_t)n) {
+                const uint32_t h = ((uint32_t)sb + er) * 2654435761u & ((1u << 26) - 1u);
+                *reinterpret_cast<u32x4 *>(T + (size_t)h * k + 4 * q) = xp[u];
+            }
+            continue;
+        }
         __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0, MAXK_T_AUX);
     }
 }
@@ -331,7 +348,7 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t t = base + u * RI + g;
-                const int e = eid[t < te ? t : tb];
+                const int e = (MAXK_BWD_ABL & 4) ? (int)(t < te ? t : tb) : eid[t < te ? t : tb];
                 v[u] = T4[(size_t)(uint32_t)e * LR + q];
                 if (t >= te) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
