@@ -95,6 +95,9 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1
 #endif
+#ifndef MAXK_CSC_STAGE  // csc phase 2: an item's csc_eid slots staged in LDS first
+#define MAXK_CSC_STAGE 1
+#endif
 #ifndef MAXK_BWD_ABL  // tuning only (wrong results): 1 phase-1 selectors from a 4096-row table, 2 no T stores but the last,
                       // 4 csc phase 2 reads T rows in order (no eid), 8 phase-1 T rows stored at hashed rows
 #define MAXK_BWD_ABL 0

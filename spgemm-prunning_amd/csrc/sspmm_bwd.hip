@@ -334,9 +334,8 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
 // dst[0:k], in a fixed order.  VEC (k in {4,8,...,256}): LR = k/4 lanes per row
 // (16-B loads), 64/LR rows per wave step, U steps in flight; the row groups are
 // combined by xor butterflies.  Scalar: KG = pow2ceil(k) lanes per row.
-template <bool VEC, int KG, int U>
-__device__ __forceinline__ void segment_sum(const float *__restrict__ T,
-                                            const int32_t *__restrict__ eid, int64_t tb,
+template <bool VEC, int KG, int U, typename EidAt>
+__device__ __forceinline__ void segment_sum(const float *__restrict__ T, EidAt eid, int64_t tb,
                                             int64_t te, int k, float *__restrict__ dst, int lane) {
     if constexpr (VEC) {
         const int LR = k / 4, RI = kWave / LR;
@@ -348,7 +347,7 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t t = base + u * RI + g;
-                const int e = (MAXK_BWD_ABL & 4) ? (int)(t < te ? t : tb) : eid[t < te ? t : tb];
+                const int e = (MAXK_BWD_ABL & 4) ? (int)(t < te ? t : tb) : eid(t < te ? t : tb);
                 v[u] = T4[(size_t)(uint32_t)e * LR + q];
                 if (t >= te) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
@@ -379,7 +378,7 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const int64_t t = base + u * G + grp;
-                    const int e = eid[t < te ? t : tb];
+                    const int e = eid(t < te ? t : tb);
                     v[u] = T[(size_t)(uint32_t)e * k + lc];
                     if (t >= te) v[u] = 0.f;
                 }
@@ -392,7 +391,13 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T,
     }
 }
 
-template <bool VEC, int KG, int U>
+// STAGED (chunk <= kCscStage): the item's CSC slots are one contiguous range of csc_eid,
+// starting at d0 - c (the tokens before d0 hold c destination tokens), so the wave copies
+// up to `chunk` of them into LDS with coalesced loads before its first segment: every T-row
+// gather then waits for one load instead of two dependent ones (a destination of ogbn-products
+// averages 50 slots, two U-steps, so each step used to wait for its eid loads first).
+constexpr int kCscStage = 2048;
+template <bool VEC, int KG, int U, bool STAGED>
 __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restrict__ col_ptr,
                                                          const int32_t *__restrict__ eid,
                                                          const float *__restrict__ T,
@@ -401,6 +406,7 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
                                                          int32_t *__restrict__ slab_row,
                                                          int num_cols, int64_t num_e, int k,
                                                          int chunk, int n_items) {
+    extern __shared__ int32_t s_eid[];  // STAGED: [kWavesPerBlock][chunk]
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
     const int blk = MAXK_XCD_SUM ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -410,13 +416,26 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
     const int64_t d0 = (int64_t)item * chunk;
     const int64_t d1 = d0 + chunk < total ? d0 + chunk : total;
     int c = wave_first_row_token(col_ptr, num_cols, d0);
+    const int64_t p_lo = d0 - c;  // the item's first CSC slot
+    int32_t *se_lds = s_eid + (STAGED ? wid * chunk : 0);
+    if constexpr (STAGED) {
+        const int n_pos = (int)(num_e - p_lo < chunk ? num_e - p_lo : chunk);
+        for (int i = lane; i < n_pos; i += kWave) se_lds[i] = eid[p_lo + i];
+        wave_lds_fence();
+    }
+    auto eid_at = [&](int64_t t) -> int {
+        if constexpr (STAGED)
+            return se_lds[(int)(t - p_lo)];
+        else
+            return eid[t];
+    };
     int cont = -1;
     if (c > 0) {
-        const int64_t sb = d0 - c;
+        const int64_t sb = p_lo;
         int64_t se = (int64_t)col_ptr[c];
         if (d1 - c < se) se = d1 - c;
         if (sb < se) {
-            segment_sum<VEC, KG, U>(T, eid, sb, se, k, slab + (int64_t)item * k, lane);
+            segment_sum<VEC, KG, U>(T, eid_at, sb, se, k, slab + (int64_t)item * k, lane);
             cont = c - 1;
         }
     }
@@ -426,7 +445,7 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
         if (cb + c >= d1) break;
         int64_t se = (int64_t)col_ptr[c + 1];
         if (d1 - c - 1 < se) se = d1 - c - 1;
-        segment_sum<VEC, KG, U>(T, eid, cb, se, k, grad_cbsr + (int64_t)c * k, lane);
+        segment_sum<VEC, KG, U>(T, eid_at, cb, se, k, grad_cbsr + (int64_t)c * k, lane);
     }
 }
 
@@ -1291,13 +1310,21 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
     const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
     const dim3 grid((unsigned)(MAXK_XCD_SUM ? xcd_grid(blocks) : blocks));
     const int nc = (int)num_cols;
+    const bool staged = MAXK_CSC_STAGE && L.chunk <= kCscStage;
+    const size_t lds = (size_t)kWavesPerBlock * L.chunk * sizeof(int32_t);
     if (vec_sum(k)) {
         const int rows_per_step = kWave / (k / 4);
         const int u = MAXK_SUM_U > 0 ? MAXK_SUM_U
                                      : pick_depth(num_e, num_cols, rows_per_step, 2, 8);
 #define MAXK_SUM_LAUNCH(UV)                                                                  \
-    hipLaunchKernelGGL((csc_sum_kernel<true, 64, UV>), grid, dim3(kBlock), 0, s, col_ptr,    \
-                       csc_eid, T, grad_cbsr, slab, slab_row, nc, num_e, k, L.chunk, L.n_items)
+    if (staged)                                                                              \
+        hipLaunchKernelGGL((csc_sum_kernel<true, 64, UV, true>), grid, dim3(kBlock), lds, s, \
+                           col_ptr, csc_eid, T, grad_cbsr, slab, slab_row, nc, num_e, k,     \
+                           L.chunk, L.n_items);                                              \
+    else                                                                                     \
+        hipLaunchKernelGGL((csc_sum_kernel<true, 64, UV, false>), grid, dim3(kBlock), 0, s,  \
+                           col_ptr, csc_eid, T, grad_cbsr, slab, slab_row, nc, num_e, k,     \
+                           L.chunk, L.n_items)
         if (u <= 2)
             MAXK_SUM_LAUNCH(2);
         else if (u <= 4)
@@ -1309,9 +1336,15 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
         switch (lanes_per_edge(k)) {
 #define MAXK_CASE(KGV)                                                                        \
     case KGV:                                                                                 \
-        hipLaunchKernelGGL((csc_sum_kernel<false, KGV, 4>), grid, dim3(kBlock), 0, s, col_ptr, \
-                           csc_eid, T,                                                        \
-                           grad_cbsr, slab, slab_row, nc, num_e, k, L.chunk, L.n_items);      \
+        if (staged)                                                                           \
+            hipLaunchKernelGGL((csc_sum_kernel<false, KGV, 4, true>), grid, dim3(kBlock), lds, \
+                               s,                                                             \
+                               col_ptr, csc_eid, T, grad_cbsr, slab, slab_row, nc, num_e, k,  \
+                               L.chunk, L.n_items);                                           \
+        else                                                                                  \
+            hipLaunchKernelGGL((csc_sum_kernel<false, KGV, 4, false>), grid, dim3(kBlock), 0, \
+                               s, col_ptr, csc_eid, T, grad_cbsr, slab, slab_row, nc, num_e,  \
+                               k, L.chunk, L.n_items);                                        \
         break;
             MAXK_CASE(1)
             MAXK_CASE(2)
