@@ -49,6 +49,28 @@ for W in (V, V // 2, V // 4, V // 8, V // 16, V // 64):
     print(f"{a.graph} k={k} forward, columns in a window of {W:7d} vertices "
           f"({W * 128 / 2**20:6.1f} MiB of records): {ms:.3f} ms", flush=True)
     del c2
+# the forward as P launches over column ranges (each launch: the edges whose column lies in
+# its range, a sub-CSR), so each launch's records are 1/P of the table
+deg_all = torch.diff(row_ptr)
+rows = torch.repeat_interleave(torch.arange(V, device=dev), deg_all.long())
+for P in (2, 4):
+    subs = []
+    for j in range(P):
+        lo, hi = V * j // P, V * (j + 1) // P
+        m = (col >= lo) & (col < hi)
+        cnt = torch.bincount(rows[m], minlength=V)
+        rp = torch.zeros(V + 1, dtype=torch.int32, device=dev)
+        rp[1:] = torch.cumsum(cnt, 0).to(torch.int32)
+        subs.append((rp, col[m].contiguous(), val[m].contiguous()))
+    tot = 0.0
+    for j, (rp, c2, v2) in enumerate(subs):
+        ms = t(lambda: mk.spgemm_forward(rp, c2, v2, cv, ci, D, out=y, validate=False))
+        tot += ms
+        print(f"  column part {j}/{P}: {c2.numel()} edges {ms:.3f} ms", flush=True)
+    print(f"{a.graph} k={k} forward as {P} column-range launches: {tot:.3f} ms "
+          f"(+ {P - 1} read-modify-writes of the output)", flush=True)
+    del subs
+del rows
 parts = torch.rand(8, V, D, device=dev)
 ms = t(lambda: torch.sum(parts, 0, out=y))
 print(f"sum of 8 partials [{V}, {D}] -> [{V}, {D}]: {ms:.3f} ms "
