@@ -18,7 +18,17 @@ where it applies:
   * lin_before_mp paths apply the Linear to the [V, k] top-k values (:166, 330)
     -> here aggregation always runs on the CBSR and the Linear after it (equal by
     linearity, and the aggregation keeps its k-sparse input);
-  * GIN "sum" passes the degrees, i.e. computes a mean (:493) -> here a sum.
+  * GIN "sum" passes the degrees, i.e. computes a mean (:493) -> here a sum;
+  * the models' feat_drop masks x_sparse but the aggregation is fed the undropped
+    topk_values (:153-181, :661-664, :743-746) -> here the aggregated values are the
+    dropped ones.
+
+`reference_compat=True` (on `maxk`, the convolutions and the models) reproduces every one of
+these behaviours instead, so a model trained with the reference computes the same function
+here (tests/test_layers_gpu.py checks each against a dense restatement of the reference's
+lines).  The reference's lin_before_mp branches (in_feats > out_feats) multiply the [V, k]
+top-k values by an [in_feats, out] matrix, which raises and sends the reference to its DGL
+fallback, i.e. the normalised aggregation; compat mode computes that fallback there.
 """
 from __future__ import annotations
 
@@ -73,23 +83,41 @@ class MaxK(Function):
     writes the whole dense row in one kernel (maxk_topk_backward)."""
 
     @staticmethod
-    def forward(ctx, x: torch.Tensor, k: int):
+    def forward(ctx, x: torch.Tensor, k: int, drop_topk_grad: bool = False):
         dense, vals, idx = mk.topk_cbsr_dense(x.float(), int(k))
         ctx.save_for_backward(idx)
         ctx.D = x.shape[1]
+        ctx.drop = bool(drop_topk_grad)
         ctx.mark_non_differentiable(idx)
         return dense, vals, idx
 
     @staticmethod
     def backward(ctx, g_dense, g_vals, g_idx):
         idx, = ctx.saved_tensors
-        gv = None if g_vals is None else g_vals.float().contiguous()
+        # drop_topk_grad: OPTMaxK.backward (model_integrated_v3.py:39-43) returns
+        # grad_output * mask and ignores the topk_values gradient
+        gv = None if g_vals is None or ctx.drop else g_vals.float().contiguous()
         gd = None if g_dense is None else g_dense.float().contiguous()
-        return mk.topk_backward(gv, gd, idx, ctx.D), None
+        if gv is None and gd is None:
+            return None, None, None
+        return mk.topk_backward(gv, gd, idx, ctx.D), None, None
 
 
-def maxk(x: torch.Tensor, k: int):
-    return MaxK.apply(x, k)
+def maxk(x: torch.Tensor, k: int, reference_compat: bool = False):
+    """(masked dense x, topk_values, topk_indices u8).  reference_compat: the topk_values
+    gradient is dropped, as the reference's OPTMaxK does."""
+    return MaxK.apply(x, k, reference_compat)
+
+
+def _dropped_values(x_sparse: torch.Tensor, topk_values: torch.Tensor,
+                    topk_indices: torch.Tensor, drop: nn.Module) -> tuple:
+    """(dropout(x_sparse), its values at the selected columns): the CBSR of the dropped
+    features, so the aggregation sees what the layer's dense input sees.  Without an
+    active dropout both are returned unchanged."""
+    if not drop.training or getattr(drop, "p", 0.0) == 0.0:
+        return x_sparse, topk_values
+    xd = drop(x_sparse)
+    return xd, xd.gather(1, topk_indices.long())
 
 
 # ---- dense parts of a full-graph layer (N = all vertices) ---------------------------------
@@ -172,9 +200,11 @@ class MaxKSAGEConv(nn.Module):
     rst = fc_self(x_sparse) + fc_neigh(mean_{u in N(v)} x_sparse[u])."""
 
     def __init__(self, in_feats: int, out_feats: int, bias: bool = True, feat_drop: float = 0.,
-                 activation=None, norm: Optional[nn.Module] = None):
+                 activation=None, norm: Optional[nn.Module] = None,
+                 reference_compat: bool = False):
         super().__init__()
         self.in_feats, self.out_feats = in_feats, out_feats
+        self.reference_compat = reference_compat
         self.fc_neigh = nn.Linear(in_feats, out_feats, bias=False)
         self.fc_self = nn.Linear(in_feats, out_feats, bias=bias)
         self.feat_drop = nn.Dropout(feat_drop)
@@ -185,9 +215,14 @@ class MaxKSAGEConv(nn.Module):
 
     def forward(self, graph: CSRGraph, x_sparse, topk_values, topk_indices):
         deg = graph.in_degrees.clamp(min=1.0)
+        if self.reference_compat:  # :153-181: only h_self sees the dropout
+            h_self = self.feat_drop(x_sparse)
+        else:
+            h_self, topk_values = _dropped_values(x_sparse, topk_values, topk_indices,
+                                                  self.feat_drop)
         agg = graph.aggregate(topk_values, topk_indices, self.in_feats, row_div=deg)
         # fc_self(x) + fc_neigh(agg) as one accumulated pair of GEMMs
-        rst = linear(self.feat_drop(x_sparse), self.fc_self, agg, self.fc_neigh)
+        rst = linear(h_self, self.fc_self, agg, self.fc_neigh)
         if self.activation is not None:
             rst = self.activation(rst)
         if self.norm is not None:
@@ -200,12 +235,13 @@ class MaxKGraphConv(nn.Module):
     norm "both" = D_in^-1/2 A D_out^-1/2, "right" = D_in^-1 A, "left" = A D_out^-1."""
 
     def __init__(self, in_feats: int, out_feats: int, norm: str = "both", weight: bool = True,
-                 bias: bool = True, activation=None):
+                 bias: bool = True, activation=None, reference_compat: bool = False):
         super().__init__()
         if norm not in ("none", "both", "right", "left"):
             raise ValueError(f'Invalid norm value. Must be either "none", "both", "right" or '
                              f'"left". But got "{norm}".')
         self.in_feats, self.out_feats, self._norm = in_feats, out_feats, norm
+        self.reference_compat = reference_compat
         self.weight = nn.Parameter(torch.empty(in_feats, out_feats)) if weight else None
         self.bias = nn.Parameter(torch.zeros(out_feats)) if bias else None
         self.activation = activation
@@ -229,10 +265,21 @@ class MaxKGraphConv(nn.Module):
         return self._edge_values
 
     def forward(self, graph: CSRGraph, x_sparse, topk_values, topk_indices):
-        rst = graph.aggregate(topk_values, topk_indices, self.in_feats,
-                              values=self._norm_values(graph))
-        if self.weight is not None:
-            rst = rst @ self.weight
+        if self.reference_compat and self.in_feats <= self.out_feats:
+            # :302-310 normalise feat_src, which the kernel never reads; :341-345 feed it the
+            # raw topk_values with the in-degrees as divisor; :381-389 then apply the right
+            # normalisation on top
+            deg = graph.in_degrees.clamp(min=1.0)
+            rst = graph.aggregate(topk_values, topk_indices, self.in_feats, row_div=deg)
+            if self.weight is not None:
+                rst = rst @ self.weight
+            if self._norm in ("right", "both"):
+                rst = rst * (deg.pow(-0.5) if self._norm == "both" else 1.0 / deg)[:, None]
+        else:
+            rst = graph.aggregate(topk_values, topk_indices, self.in_feats,
+                                  values=self._norm_values(graph))
+            if self.weight is not None:
+                rst = rst @ self.weight
         if self.bias is not None:
             rst = rst + self.bias
         if self.activation is not None:
@@ -245,16 +292,19 @@ class MaxKGINConv(nn.Module):
     rst = apply_func((1 + eps) x + sum_{u in N(v)} x_sparse[u])."""
 
     def __init__(self, apply_func: Optional[nn.Module] = None, init_eps: float = 0.,
-                 learn_eps: bool = False, activation=None):
+                 learn_eps: bool = False, activation=None, reference_compat: bool = False):
         super().__init__()
         self.apply_func, self.activation = apply_func, activation
+        self.reference_compat = reference_compat
         if learn_eps:
             self.eps = nn.Parameter(torch.tensor([float(init_eps)]))
         else:
             self.register_buffer("eps", torch.tensor([float(init_eps)]))
 
     def forward(self, graph: CSRGraph, x, topk_values, topk_indices):
-        neigh = graph.aggregate(topk_values, topk_indices, x.shape[1])
+        # reference_compat: the "sum" kernel call passes the in-degrees (:491-495), a mean
+        row_div = graph.in_degrees.clamp(min=1.0) if self.reference_compat else None
+        neigh = graph.aggregate(topk_values, topk_indices, x.shape[1], row_div=row_div)
         rst = (1 + self.eps) * x + neigh
         if self.apply_func is not None:
             rst = self.apply_func(rst)
@@ -264,22 +314,103 @@ class MaxKGINConv(nn.Module):
 
 
 class MaxKSAGE(nn.Module):
-    """lin_in -> [MaxK -> MaxKSAGEConv] x L -> lin_out (model_integrated_v3.py:522-588)."""
+    """lin_in -> [MaxK -> MaxKSAGEConv] x L -> lin_out (model_integrated_v3.py:522-588; same
+    constructor arguments; graph_name is accepted and unused: no schedule files are needed)."""
 
-    def __init__(self, in_size: int, hid_size: int, out_size: int, num_layers: int = 3,
-                 maxk: int = 32, feat_drop: float = 0., norm: bool = False):
+    def __init__(self, in_size: int, hid_size: int, num_hid_layers: int, out_size: int,
+                 maxk: int = 32, feat_drop: float = 0.5, norm: bool = False,
+                 nonlinear: str = "maxk", graph_name: str = "", reference_compat: bool = False):
         super().__init__()
-        self.k = maxk
+        if nonlinear != "maxk":
+            raise ValueError(f"Only 'maxk' supported, got {nonlinear}")
+        self.k, self.num_layers, self.graph_name = maxk, num_hid_layers, graph_name
+        self.reference_compat = reference_compat
         self.lin_in = nn.Linear(in_size, hid_size)
         self.layers = nn.ModuleList([
             MaxKSAGEConv(hid_size, hid_size, feat_drop=feat_drop,
-                         norm=nn.LayerNorm(hid_size) if norm else None)
-            for _ in range(num_layers)])
+                         norm=nn.LayerNorm(hid_size) if norm else None,
+                         reference_compat=reference_compat)
+            for _ in range(num_hid_layers)])
         self.lin_out = nn.Linear(hid_size, out_size)
+        nn.init.xavier_uniform_(self.lin_in.weight)
+        nn.init.xavier_uniform_(self.lin_out.weight)
 
     def forward(self, graph: CSRGraph, x):
         x = linear(x, self.lin_in)
         for layer in self.layers:
-            x_sparse, vals, idx = maxk(x, self.k)
+            x_sparse, vals, idx = maxk(x, self.k, self.reference_compat)
             x = layer(graph, x_sparse, vals, idx)
         return linear(x, self.lin_out)
+
+
+class _MaxKStack(nn.Module):
+    """Shared body of MaxKGCN / MaxKGIN (model_integrated_v3.py:590-752): lin_in + relu, then
+    per layer Linear -> MaxK -> dropout -> conv (-> LayerNorm), then lin_out."""
+
+    def __init__(self, in_size, hid_size, num_hid_layers, out_size, maxk, feat_drop, norm,
+                 nonlinear, graph_name, reference_compat, make_conv):
+        super().__init__()
+        if nonlinear != "maxk":
+            raise ValueError(f"Only 'maxk' supported, got {nonlinear}")
+        self.k, self.num_layers, self.graph_name = maxk, num_hid_layers, graph_name
+        self.reference_compat = reference_compat
+        self.dropoutlayers = nn.ModuleList([nn.Dropout(feat_drop) for _ in range(num_hid_layers)])
+        self.convs = nn.ModuleList([make_conv() for _ in range(num_hid_layers)])
+        self.normlayers = nn.ModuleList([nn.LayerNorm(hid_size) for _ in range(num_hid_layers)]
+                                        if norm else [])
+        self.linlayers = nn.ModuleList([nn.Linear(hid_size, hid_size)
+                                        for _ in range(num_hid_layers)])
+        for lin in self.linlayers:
+            nn.init.xavier_uniform_(lin.weight)
+        self.lin_in = nn.Linear(in_size, hid_size)
+        self.lin_out = nn.Linear(hid_size, out_size)
+        nn.init.xavier_uniform_(self.lin_in.weight)
+        nn.init.xavier_uniform_(self.lin_out.weight)
+
+    def forward(self, graph: CSRGraph, x):
+        x = linear(x, self.lin_in).relu()
+        for i in range(self.num_layers):
+            x = linear(x, self.linlayers[i])
+            x_sparse, vals, idx = maxk(x, self.k, self.reference_compat)
+            if self.reference_compat:  # :661, :743: the kernel gets the undropped values
+                x_sparse = self.dropoutlayers[i](x_sparse)
+            else:
+                x_sparse, vals = _dropped_values(x_sparse, vals, idx, self.dropoutlayers[i])
+            x = self.convs[i](graph, x_sparse, vals, idx)
+            if self.normlayers:
+                x = self.normlayers[i](x)
+        return linear(x, self.lin_out)
+
+
+class MaxKGCN(_MaxKStack):
+    """GCN model (model_integrated_v3.py:590-670): MaxKGraphConv(norm="both", no weight, no
+    bias) after a per-layer Linear."""
+
+    def __init__(self, in_size: int, hid_size: int, num_hid_layers: int, out_size: int,
+                 maxk: int = 32, feat_drop: float = 0.5, norm: bool = False,
+                 nonlinear: str = "maxk", graph_name: str = "", reference_compat: bool = False):
+        super().__init__(in_size, hid_size, num_hid_layers, out_size, maxk, feat_drop, norm,
+                         nonlinear, graph_name, reference_compat,
+                         lambda: MaxKGraphConv(hid_size, hid_size, norm="both", weight=False,
+                                               bias=False, reference_compat=reference_compat))
+
+    @property
+    def gcnlayers(self):
+        return self.convs
+
+
+class MaxKGIN(_MaxKStack):
+    """GIN model (model_integrated_v3.py:672-752): MaxKGINConv(sum, learnable eps from 0)
+    after a per-layer Linear."""
+
+    def __init__(self, in_size: int, hid_size: int, num_hid_layers: int, out_size: int,
+                 maxk: int = 32, feat_drop: float = 0.5, norm: bool = False,
+                 nonlinear: str = "maxk", graph_name: str = "", reference_compat: bool = False):
+        super().__init__(in_size, hid_size, num_hid_layers, out_size, maxk, feat_drop, norm,
+                         nonlinear, graph_name, reference_compat,
+                         lambda: MaxKGINConv(None, init_eps=0.0, learn_eps=True,
+                                             reference_compat=reference_compat))
+
+    @property
+    def ginlayers(self):
+        return self.convs

@@ -142,8 +142,8 @@ def main(argv=None):
     x = torch.randn(V, f_in, generator=gen, device=dev)
     y = torch.randint(0, n_cls, (V,), generator=gen, device=dev)
     torch.manual_seed(0)
-    model = maxk_layers.MaxKSAGE(f_in, args.hidden, n_cls, num_layers=args.layers,
-                                 maxk=args.k).to(dev)
+    model = maxk_layers.MaxKSAGE(f_in, args.hidden, args.layers, n_cls, maxk=args.k,
+                                 feat_drop=0.0).to(dev)
     ref = copy.deepcopy(model)
     ms, loss0 = time_epochs(model, g, x, y, args.epochs, args.warmup)
     out = {"graph": args.graph, "source": source, "V": V, "E": indices.numel(),
