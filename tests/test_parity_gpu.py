@@ -305,7 +305,9 @@ def test_all_k_against_oracle(mk, cuda, k, D):
     cv, ci = O.topk(x, k)
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-    modes = [(0, "auto"), (0, "csc"), (13, "csc"), (13, "atomic")]
+    # csc: chunk 2048 is the largest item whose eid slots are staged in LDS, 4096 reads them
+    # from global memory (csc_sum_kernel STAGED)
+    modes = [(0, "auto"), (0, "csc"), (13, "csc"), (2048, "csc"), (4096, "csc"), (13, "atomic")]
     if k % 4 == 0:
         modes.append((13, "bucket"))
     if D % 4 == 0 and (k % 4 == 0 or k <= 64):
