@@ -208,7 +208,15 @@ class ShardedMaxK:
         recv = torch.empty(sum(self.send_counts), k, dtype=partial.dtype, device=partial.device)
         _all_to_all(recv, partial.contiguous(), self.send_counts, self.recv_counts, self.group)
         out = torch.zeros(self.n_local, k, dtype=partial.dtype, device=partial.device)
-        return out.index_add_(0, self.send_rows.to(partial.device), recv)
+        # one index_add per requester, in rank order: a requester's rows are distinct, so no
+        # add races another and the sum order is fixed (run to run bitwise)
+        rows = self.send_rows.to(partial.device)
+        o = 0
+        for n in self.send_counts:
+            if n:
+                out.index_add_(0, rows[o:o + n], recv[o:o + n])
+            o += n
+        return out
 
     def plan(self, k: int, D: Optional[int] = None):
         """The backward's per-graph plan at width k and feature width D (built once per
