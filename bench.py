@@ -225,6 +225,9 @@ def main():
     ap.add_argument("--graph-dir", default=None,
                     help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
     ap.add_argument("--no-cpu-spmm", action="store_true")
+    ap.add_argument("--reorder", action="store_true",
+                    help="relabel the graph once by maxk_graph.locality_order (communities "
+                         "contiguous) before sharding and timing")
     ap.add_argument("--dist-mode", default="gather", choices=["gather", "halo"],
                     help="N > 1: all-gather every CBSR row, or exchange only the halo rows")
     args = ap.parse_args()
@@ -271,7 +274,6 @@ def main():
     D = args.dim or P["D"]
     k = args.k or P["k"]
     V = P["V"]
-    E_target = P["E"] - ((P["E"] - V) % 2)
     t0 = time.time()
     gdir = maxk_graph.find_graph(args.graph, [args.graph_dir] if args.graph_dir else [])
     if gdir:
@@ -281,13 +283,16 @@ def main():
         V = g["v_num"]
         data = f"real graph {gdir}/{args.graph}.indptr|.indices; synthetic features"
     elif world == 1:
-        row_ptr, col = maxk_graph.make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
+        row_ptr, col = maxk_graph.synthetic_graph(args.graph, args.seed, dev)
         data = "synthetic"
     else:
         # one rank builds the graph, the others receive it (one broadcast of row_ptr + col)
         cdev = dev if backend == "nccl" else torch.device("cpu")
         if rank == 0:
-            row_ptr, col = maxk_graph.make_graph(V, E_target, P["alpha"], P["i0"], args.seed, dev)
+            row_ptr, col = maxk_graph.synthetic_graph(args.graph, args.seed, dev)
+            if args.reorder:
+                row_ptr, col, _ = maxk_graph.permute_graph(
+                    row_ptr, col, maxk_graph.locality_order(row_ptr, col))
             n_e = torch.tensor([col.numel()], dtype=torch.int64, device=cdev)
         else:
             n_e = torch.zeros(1, dtype=torch.int64, device=cdev)
@@ -303,6 +308,16 @@ def main():
                 dist.broadcast(h, 0)
                 t.copy_(h)
         data = "synthetic (built on rank 0, broadcast)"
+    t_reorder = None
+    if args.reorder:
+        if world == 1:
+            torch.cuda.synchronize()
+            t_r = time.perf_counter()
+            row_ptr, col, _ = maxk_graph.permute_graph(
+                row_ptr, col, maxk_graph.locality_order(row_ptr, col))
+            torch.cuda.synchronize()
+            t_reorder = time.perf_counter() - t_r
+        data += "; vertex order by maxk_graph.locality_order (once per graph, untimed)"
     E = col.numel()
     gen = torch.Generator(device=dev).manual_seed(123)  # kernels/main.cu:74-77 seed
     val = torch.rand(E, generator=gen, device=dev)
@@ -346,7 +361,7 @@ def main():
     # one validated call (row_ptr/col_idx/selector ranges) before the raw timed launches
     mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, validate=True)
     # per-graph setup (like the reference's warp4 files): the backward's bucket / transpose plan
-    args.bwd_mode = mk._bwd_mode(args.bwd_mode, k, El, n_cols, nl, D)  # "auto" -> the mode that runs
+    args.bwd_mode = mk._bwd_mode(args.bwd_mode, k, El, n_cols, nl, D, l_row_ptr, l_col)  # "auto" -> the mode that runs
     torch.cuda.synchronize()
     t_plan = time.perf_counter()
     plan = mk.backward_plan(l_col, n_cols, k, args.bwd_mode, indptr=l_row_ptr, values=l_val, dim=D)
@@ -445,6 +460,11 @@ def main():
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
         "bwd_mode": args.bwd_mode, "backward_plan_s": round(t_plan, 4),
     }
+    if args.reorder:
+        extra["reorder_s"] = None if t_reorder is None else round(t_reorder, 3)
+    # edges per occupied (source row, pull bucket): the locality the pull backward feeds on
+    extra["pull_locality"] = round(
+        mk.pull_locality(l_row_ptr, l_col, int(mk._lib().maxk_pull_shift(k))), 3)
     f_traffic, _ = load_traffic(tkey, "spgemm_forward")
     if f_traffic:  # forward: measured (PMC) bytes per launch over its live duration
         extra["fwd_traffic_GB"] = round(f_traffic / 1e9, 3)

@@ -14,7 +14,11 @@ sorted column indices, which the reference's DGL `adj_tensors('csr')` does not
 promise (the kernels accept either).
 
 `synthetic_graph` / `PRESETS`: the stand-ins used when the real files are absent
-(symmetric Chung-Lu power law with self loops at the published V and E).
+(symmetric Chung-Lu power law with self loops at the published V and E).  They are randomly
+labelled, so they have no locality at all; `community_graph` adds planted communities (the
+structure real graphs such as ogbn-products have), and `locality_order` / `permute_graph`
+find and apply a vertex order that makes such structure contiguous (once per graph, like the
+reference's offline .warp4 files).
 """
 from __future__ import annotations
 
@@ -139,6 +143,10 @@ def find_graph(name: str, dirs=None) -> Optional[str]:
 PRESETS = {
     "reddit": dict(V=232_965, E=114_615_891, alpha=0.7, i0=200, D=256, k=16),
     "products": dict(V=2_449_029, E=123_718_280, alpha=0.75, i0=3000, D=256, k=32),
+    # ogbn-products' size and degree skew with planted communities (~1,200 vertices each,
+    # 90 % of the edges inside one), randomly labelled: the locality a real graph has, hidden
+    "products_comm": dict(V=2_449_029, E=123_718_280, alpha=0.75, i0=3000, D=256, k=32,
+                          communities=2_000, p_in=0.9),
     "proteins": dict(V=132_534, E=79_122_504, alpha=0.45, i0=2000, D=256, k=64),
     "flickr": dict(V=89_250, E=989_006, alpha=0.9, i0=30, D=64, k=16),
 }
@@ -198,8 +206,118 @@ def make_graph(V, E, alpha, i0, seed, device, trace=None):
 
 def synthetic_graph(name: str, seed: int = 1, device="cuda"):
     """(row_ptr int32, col int32) of the synthetic stand-in for a published graph: its exact V,
-    E (E - V made even) and a degree skew like the real one."""
+    E (E - V made even) and a degree skew like the real one; presets with
+    `communities` plant them (community_graph)."""
     P = PRESETS[name]
     V = P["V"]
     E = P["E"] - ((P["E"] - V) % 2)
+    if "communities" in P:
+        return community_graph(V, E, P["alpha"], P["i0"], P["communities"], P["p_in"], seed,
+                               torch.device(device))
     return make_graph(V, E, P["alpha"], P["i0"], seed, torch.device(device))
+
+
+def _csr_from_pairs(lo: torch.Tensor, hi: torch.Tensor, V: int):
+    """Symmetric CSR (sorted columns) of the undirected pairs lo < hi plus a self loop on
+    every vertex."""
+    loops = torch.arange(V, device=lo.device)
+    src = torch.cat([lo, hi, loops])
+    dst = torch.cat([hi, lo, loops])
+    key = torch.sort(src * V + dst).values
+    del src, dst
+    src, dst = key // V, key % V
+    row_ptr = torch.zeros(V + 1, dtype=torch.int64, device=lo.device)
+    row_ptr[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)
+    return row_ptr.to(torch.int32), dst.to(torch.int32)
+
+
+def community_graph(V, E, alpha, i0, communities, p_in, seed, device):
+    """Symmetric graph with planted communities, self loops, exactly E edges (E - V even).
+
+    Vertex weights follow make_graph's power law, assigned to vertices in random order;
+    communities are `communities` equal blocks of that order.  Each undirected pair takes
+    one endpoint by weight and the other, with probability p_in, uniformly from the first
+    one's community, else by weight from the whole graph.  A final random relabelling
+    hides the blocks, as a dataset's arbitrary vertex ids would."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    pairs_target = (E - V) // 2
+    w = (torch.arange(V, device=device, dtype=torch.float64) + i0) ** (-alpha)
+    w = w[torch.randperm(V, generator=g, device=device)]  # hubs spread over the communities
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    size = -(-V // communities)
+    keys = torch.empty(0, dtype=torch.int64, device=device)
+    need = pairs_target
+    while keys.numel() < pairs_target:
+        m = int(need * 1.25) + 4096
+        a = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device,
+                                               dtype=torch.float64)).clamp_(max=V - 1)
+        b = torch.searchsorted(cdf, torch.rand(m, generator=g, device=device,
+                                               dtype=torch.float64)).clamp_(max=V - 1)
+        inside = torch.rand(m, generator=g, device=device) < p_in
+        c0 = a // size * size
+        span = torch.clamp(V - c0, max=size)
+        bc = c0 + (torch.rand(m, generator=g, device=device, dtype=torch.float64) * span).long()
+        b = torch.where(inside, bc.clamp_(max=V - 1), b)
+        lo, hi = torch.minimum(a, b), torch.maximum(a, b)
+        k = (lo * V + hi)[lo != hi]
+        keys = torch.unique(torch.cat([keys, k]))
+        need = pairs_target - keys.numel()
+        del a, b, inside, c0, span, bc, lo, hi, k
+    keys = keys[torch.randperm(keys.numel(), generator=g, device=device)[:pairs_target]]
+    relabel = torch.randperm(V, generator=g, device=device)
+    lo, hi = relabel[keys // V], relabel[keys % V]
+    del keys
+    return _csr_from_pairs(lo, hi, V)
+
+
+def locality_order(indptr: torch.Tensor, indices: torch.Tensor, iters: int = 20,
+                   seed: int = 0) -> torch.Tensor:
+    """A vertex order that makes a graph's communities contiguous: `perm[new] = old`.
+
+    Label propagation on the device (each round a random half of the vertices takes the most
+    frequent label among its neighbours, its own counted through the self loop; ties go to
+    a per-round random hash of the label, so no label floods by id, and updating half the
+    vertices per round keeps neighbours from swapping labels back and forth), then vertices
+    sorted by (label, old id).  Once per graph; apply with permute_graph.  On a randomly
+    labelled graph without structure it returns an arbitrary order and costs nothing later."""
+    V = indptr.numel() - 1
+    dev = indices.device
+    rows = torch.repeat_interleave(torch.arange(V, device=dev), torch.diff(indptr.long()))
+    cols = indices.long()
+    lab = torch.arange(V, device=dev)
+    g = torch.Generator(device=dev).manual_seed(seed)
+    for _ in range(iters):
+        h = torch.randint(0, 1 << 20, (V,), generator=g, device=dev)  # tie-break hash per label
+        uniq, cnt = torch.unique(rows * V + lab[cols], return_counts=True)
+        r, lb = uniq // V, uniq % V
+        score = (cnt << 20) | h[lb]
+        del uniq, cnt
+        best = torch.full((V,), -1, dtype=torch.int64, device=dev).scatter_reduce_(
+            0, r, score, "amax", include_self=True)
+        cand = torch.where(score == best[r], lb, torch.full_like(lb, V))
+        new = torch.full((V,), V, dtype=torch.int64, device=dev).scatter_reduce_(
+            0, r, cand, "amin", include_self=True)
+        move = (torch.rand(V, generator=g, device=dev) < 0.5) & (new < V)
+        new = torch.where(move, new, lab)
+        del r, lb, score, cand, best, move
+        lab = new
+    return torch.argsort(lab * V + torch.arange(V, device=dev))
+
+
+def permute_graph(indptr: torch.Tensor, indices: torch.Tensor, perm: torch.Tensor):
+    """The CSR of the graph relabelled by `perm` (perm[new] = old): row and column i of the
+    result are vertex perm[i].  Returns (indptr int32, indices int32, edge_perm int64) with
+    sorted columns; edge_perm[e'] is the old edge id of new edge e' (values_new =
+    values[edge_perm]).  Features follow with x[perm], outputs go back with y[inv]."""
+    V = indptr.numel() - 1
+    dev = indices.device
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(V, device=dev)
+    rows = torch.repeat_interleave(torch.arange(V, device=dev), torch.diff(indptr.long()))
+    key = inv[rows] * V + inv[indices.long()]
+    key, eperm = torch.sort(key)
+    src, dst = key // V, key % V
+    ip = torch.zeros(V + 1, dtype=torch.int64, device=dev)
+    ip[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)
+    return ip.to(torch.int32), dst.to(torch.int32), eperm

@@ -124,3 +124,64 @@ def test_kernel_test_cli(cuda, capsys):
     assert out[1].startswith("1/1 flickr 64 16 cusparse ")
     assert [r["k"] for r in res] == [16, 32]
     assert all(r["max_rel_err"] < 1e-3 and r["maxk_ms"] > 0 for r in res)
+
+
+# ---- planted communities and the locality order (maxk_graph.community_graph etc.) ----------
+
+def test_community_graph_shape():
+    import maxk_graph
+    V, E = 3000, 3000 + 2 * 30000
+    ip, ix = maxk_graph.community_graph(V, E, 0.75, 30, 10, 0.9, 1, torch.device("cpu"))
+    assert ip.numel() == V + 1 and int(ip[-1]) == E == ix.numel()
+    rows = torch.repeat_interleave(torch.arange(V), torch.diff(ip.long()))
+    key = rows * V + ix.long()
+    assert bool((key[1:] > key[:-1]).all())  # sorted columns, no multi-edges
+    rev = torch.sort(ix.long() * V + rows).values
+    assert torch.equal(rev, key)  # symmetric
+    assert int((rows == ix.long()).sum()) == V  # one self loop per vertex
+
+
+def test_permute_graph_relabels_rows_columns_and_values():
+    import maxk_graph
+    g = torch.Generator().manual_seed(3)
+    V = 200
+    ip, ix = maxk_graph.build_csr(torch.randint(0, V, (900,), generator=g),
+                                  torch.randint(0, V, (900,), generator=g), V)
+    val = torch.rand(ix.numel(), generator=g)
+    perm = torch.randperm(V, generator=g)
+    ip2, ix2, ep = maxk_graph.permute_graph(ip, ix, perm)
+
+    def dense(p, x, v):
+        A = torch.zeros(V, V)
+        A[torch.repeat_interleave(torch.arange(V), torch.diff(p.long())), x.long()] = v
+        return A
+    A, A2 = dense(ip, ix, val), dense(ip2, ix2, val[ep])
+    assert torch.equal(A2, A[perm][:, perm])  # row/column i of the result is vertex perm[i]
+
+
+def test_locality_order_groups_planted_communities():
+    import maxk_graph
+    V, E, C = 4000, 4000 + 2 * 60000, 8
+    ip, ix = maxk_graph.community_graph(V, E, 0.75, 30, C, 0.95, 2, torch.device("cpu"))
+    perm = maxk_graph.locality_order(ip, ix)
+    assert torch.equal(torch.sort(perm).values, torch.arange(V))
+    ip2, ix2, _ = maxk_graph.permute_graph(ip, ix, perm)
+    rows = torch.repeat_interleave(torch.arange(V), torch.diff(ip.long()))
+    rows2 = torch.repeat_interleave(torch.arange(V), torch.diff(ip2.long()))
+    near = lambda r, c: float(((r - c.long()).abs() < V // C).float().mean())  # noqa: E731
+    assert near(rows2, ix2) > 0.85 > 0.35 > near(rows, ix)
+
+
+def test_pull_locality():
+    import maxk_cuda_kernels as mk
+    import maxk_graph
+    V, E = 4000, 4000 + 2 * 60000
+    ip, ix = maxk_graph.community_graph(V, E, 0.75, 30, 8, 0.95, 2, torch.device("cpu"))
+    rnd = mk.pull_locality(ip, ix, 7)
+    ip2, ix2, _ = maxk_graph.permute_graph(ip, ix, maxk_graph.locality_order(ip, ix))
+    ordered = mk.pull_locality(ip2, ix2, 7)
+    assert ordered > 2 * rnd
+    # one row, columns 0..9 and 200..204 -> buckets of 128: {0}, {1}: 15 edges in 2 pairs
+    one = torch.tensor([0, 15], dtype=torch.int32)
+    cols = torch.tensor(list(range(10)) + list(range(200, 205)), dtype=torch.int32)
+    assert mk.pull_locality(one, cols, 7) == 7.5

@@ -5,7 +5,9 @@ synthetic graphs (CPU), N = 2/4/8 vertex-range shards balanced by nnz (balanced_
           a [world * vmax, k] fp32 partial: each rank receives (world-1) * vmax rows forward
           and sends as many k x 4 B rows backward.
   halo:   only the rows a shard's edges touch (its distinct remote columns) travel, each way.
-    python tools/halo_bytes.py [--graph products] [--k 32]"""
+    python tools/halo_bytes.py [--graph products] [--k 32] [--reorder]
+--reorder relabels the graph by maxk_graph.locality_order first (a planted-community graph,
+--graph products_comm, then keeps most edges inside a shard)."""
 import argparse
 import os
 import sys
@@ -21,11 +23,17 @@ import maxk_graph  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--graph", default="products")
 ap.add_argument("--k", type=int, default=None)
+ap.add_argument("--reorder", action="store_true")
+ap.add_argument("--device", default="cpu")
 a = ap.parse_args()
 k = a.k or maxk_graph.PRESETS[a.graph]["k"]
-rp, col = maxk_graph.synthetic_graph(a.graph, device="cpu")
+rp, col = maxk_graph.synthetic_graph(a.graph, device=a.device)
+if a.reorder:
+    rp, col, _ = maxk_graph.permute_graph(rp, col, maxk_graph.locality_order(rp, col))
+rp, col = rp.cpu(), col.cpu()
 V, E = rp.numel() - 1, col.numel()
-print(f"{a.graph} (synthetic) V={V} E={E} k={k}: MB per rank and step (max over ranks), "
+print(f"{a.graph} (synthetic{', locality order' if a.reorder else ''}) V={V} E={E} k={k}: "
+      f"MB per rank and step (max over ranks), "
       f"forward receive + backward send")
 for world in (2, 4, 8):
     b = maxk_dist.balanced_bounds(rp, world)
