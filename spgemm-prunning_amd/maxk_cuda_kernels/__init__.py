@@ -374,7 +374,8 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
     (row, bucket) on average has a / (1 - e^-a) (ogbn-products-sized: ~1.0); a graph whose
     vertex order groups its communities (maxk_graph.locality_order) has many more, whatever
     the average.  One pass over the edges (columns sorted within rows, else an under-
-    estimate), cached per (indptr, indices, shift) and their versions."""
+    estimate), cached per (indptr, indices, shift) and their versions.  Reported by bench.py
+    (extra.pull_locality); it does not steer mode "auto" (see _bwd_mode)."""
     key = (id(indptr), id(indices), int(shift))
     hit = _LOCALITY.get(key)
     if hit is not None:
@@ -401,9 +402,7 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
 
 
 def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0,
-              num_rows: Optional[int] = None, dim: Optional[int] = None,
-              indptr: Optional[torch.Tensor] = None,
-              indices: Optional[torch.Tensor] = None) -> str:
+              num_rows: Optional[int] = None, dim: Optional[int] = None) -> str:
     """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) picks "pull"
     where it measured faster than "csc": k % 4 == 0 or k <= 64, dim % 4 == 0 when dim is
     given, and at
@@ -411,10 +410,10 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
     (Reddit k=16: 2.2, k=64: 0.54; ogbn-proteins k=64: 1.2; ogbn-products: 0.02), or a
     gradient G of at most 64 MiB (num_rows x dim x 4 B; Flickr: 23 MB, 0.05 vs 0.13 ms), which
     stays cache-resident however sparse the graph; for more than 256 x 65536 rows "bucket"
-    (k <= 16) stands in.  Given the graph (indptr, indices) and a sparse average, "pull" is
-    still picked when its edges crowd into few (row, bucket) pairs (pull_locality >= 4: a
-    community-ordered graph; the randomly labelled ones sit near 1).  "bucket" (two-phase
-    with the same fp64 accumulator) stays selectable."""
+    (k <= 16) stands in.  Locality (pull_locality) does not enter: where the average is
+    sparse the pull's per-slice partials ([num_cols, k] per row slice) already outweigh it
+    (a community-ordered ogbn-products-sized graph: 46 ms against 8 ms csc).
+    "bucket" (two-phase with the same fp64 accumulator) stays selectable."""
     mode = mode or os.environ.get("MAXK_BWD_MODE", "auto")
     if mode not in BWD_MODES:
         raise RuntimeError(f"backward mode must be one of {BWD_MODES}, got {mode!r}")
@@ -425,10 +424,6 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
             rows = num_rows if num_rows else num_cols
             dense = num_e * (1 << shift) >= rows * num_cols // 2
             small = dim is not None and rows * dim * 4 <= (64 << 20)
-            if not (dense or small) and indptr is not None and indices is not None and \
-                    rows <= 256 * 65536 and not torch.cuda.is_current_stream_capturing():
-                pshift = int(_lib().maxk_pull_shift(int(k)))
-                dense = pull_locality(indptr, indices, pshift) >= 4.0
             if (dense or small) and rows <= 256 * 65536:
                 mode = "pull"
             elif dense and k <= 16 and k % 4 == 0:
@@ -448,7 +443,7 @@ def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[s
     """The per-graph plan sspmm_backward needs for `mode` at width k (None for "atomic");
     num_rows (default num_cols) and dim only steer mode "auto".  Mode "pull" also needs
     the graph's indptr and edge values."""
-    mode = _bwd_mode(mode, k, indices.numel(), num_cols, num_rows, dim, indptr, indices)
+    mode = _bwd_mode(mode, k, indices.numel(), num_cols, num_rows, dim)
     if mode == "pull":
         if indptr is None or values is None:
             raise RuntimeError("backward_plan: mode 'pull' needs indptr= and values=")
@@ -501,7 +496,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             raise RuntimeError("out must be [num_cols, k]")
     L = _lib()
     E = indices.numel()
-    mode = _bwd_mode(mode, k, E, num_cols, num_rows, D, indptr, indices)
+    mode = _bwd_mode(mode, k, E, num_cols, num_rows, D)
     if mode == "pull":
         tptr, ent, shift, S = (plan if plan is not None else
                                pull_plan(indptr, indices, values, num_cols, k, D))
