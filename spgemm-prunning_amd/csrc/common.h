@@ -95,6 +95,12 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1
 #endif
+#ifndef MAXK_FWD_XCD  // forward items in XCD-contiguous order
+#define MAXK_FWD_XCD 1  // Reddit / products neutral, ordered products_comm 4.71 -> 3.65 ms
+#endif
+#ifndef MAXK_P1_XCD  // backward phase 1 items in XCD-contiguous order
+#define MAXK_P1_XCD 1  // products_comm ordered 8.47 -> 8.39 ms, random graphs neutral
+#endif
 #ifndef MAXK_CSC_STAGE  // csc phase 2: an item's csc_eid slots staged in LDS first
 #define MAXK_CSC_STAGE 1
 #endif

@@ -301,7 +301,10 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int item = blockIdx.x * kWavesPerBlock + wid;
+    // MAXK_FWD_XCD: XCD x runs the x-th eighth of the items (contiguous rows), so a graph
+    // whose vertex order keeps neighbours close finds their records in that XCD's L2
+    const int blk = MAXK_FWD_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int item = blk * kWavesPerBlock + wid;
     if (item >= n_items) return;  // whole wave; no workgroup barrier below
     float *acc = lds + (size_t)wid * NC * DS;
     for (int j = lane * 4; j < NC * DS; j += kWave * 4)
@@ -433,7 +436,8 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
     constexpr int U = MAXK_FWD_U;
     constexpr int NC = kWave / KG;
     const size_t lds = (size_t)kWavesPerBlock * NC * L.DS * sizeof(float);
-    const dim3 grid((unsigned)ceil_div(L.n_items, kWavesPerBlock));
+    const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
+    const dim3 grid((unsigned)(MAXK_FWD_XCD ? xcd_grid(blocks) : blocks));
     // 32-bit record offsets need c < 2^24 (24-bit multiply) and the table under 4 GiB
     const int64_t num_cols = (int64_t)(L.rec_bytes / L.RS);
     if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32))

@@ -270,7 +270,10 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kMaxDim];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int item = blockIdx.x * kWavesPerBlock + wid;
+    // MAXK_P1_XCD: XCD-contiguous items, as in the forward (an ordered graph's destinations,
+    // whose selectors every edge reads, then stay close within one XCD)
+    const int blk = MAXK_P1_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int item = blk * kWavesPerBlock + wid;
     if (item >= n_items) return;
     float *g_lds = lds[wid];
     *reinterpret_cast<float4 *>(&g_lds[lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1137,7 +1140,8 @@ int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 const uint8_t *cbsr_idx, float *dst, int nr, int64_t num_cols, int64_t num_e,
                 int D, int k, int chunk) {
     const int n_items = n_items_for(nr, num_e, chunk);
-    const dim3 grid((unsigned)ceil_div(n_items, kWavesPerBlock));
+    const int64_t blocks = ceil_div(n_items, kWavesPerBlock);
+    const dim3 grid((unsigned)(MAXK_P1_XCD ? xcd_grid(blocks) : blocks));
     if (MODE == kStore && MAXK_BWD_X4 && k % 4 == 0) {
         const int lr = lanes_per_edge(k / 4);
         const int u = MAXK_X4_U > 0 ? MAXK_X4_U : pick_depth(num_e, nr, kWave / lr, 4, 16);
