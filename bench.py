@@ -47,6 +47,10 @@ OP_KERNELS = {
                             "pull_reduce_kernel", "gprime_kernel"],
     "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
+    # csc over the sparse tiles' edges, then the pull over the dense ones, accumulating
+    "sspmm_backward_hybrid": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>",
+                              "pull_sel_kernel", "pull_q_kernel", "pull_reduce_kernel",
+                              "gprime_kernel"],
 }
 
 
@@ -221,7 +225,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "pull", "bucket", "csc", "atomic"])
+    ap.add_argument("--bwd-mode", default="auto",
+                    choices=["auto", "pull", "bucket", "csc", "atomic", "hybrid"])
     ap.add_argument("--graph-dir", default=None,
                     help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
     ap.add_argument("--no-cpu-spmm", action="store_true")

@@ -180,6 +180,28 @@ int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
                              int32_t dim_origin, int32_t dim_k, void *workspace,
                              size_t workspace_bytes, void *stream);
 
+/* The pull over a listed subset of a plan's tiles (dim_k % 4 == 0), for graphs where only
+ * some tiles are dense enough to pull (a community-ordered graph: the tiles near the
+ * diagonal) and the rest of the edges go through the two-phase backward (the "hybrid" mode
+ * of the Python binding).  tile_list[n_tiles]: tile ids t = s*nb + j, increasing;
+ * tile_ent[n_tiles + 1]: their entry ranges in ent; bucket_ptr[nb + 1] / bucket_tiles[n_tiles]:
+ * per bucket, the positions in tile_list of its tiles in slice order.  accumulate != 0 adds
+ * the result onto grad_cbsr (which then holds the other edges' sum), else stores it.  The
+ * workspace holds n_tiles tile partials: maxk_sspmm_backward_pull_tiles_workspace_size.
+ * Replaces the same reference kernels as maxk_sspmm_backward (spmm_maxk_backward.cu:15-121). */
+size_t maxk_sspmm_backward_pull_tiles_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                     int32_t dim_origin, int32_t dim_k,
+                                                     int32_t n_tiles);
+int maxk_sspmm_backward_pull_tiles(const float *grad_out, const float *row_div,
+                                   const uint8_t *cbsr_idx, const int32_t *tile_list,
+                                   const int32_t *tile_ent, int32_t n_tiles,
+                                   const int32_t *bucket_ptr, const int32_t *bucket_tiles,
+                                   const uint32_t *ent, int32_t bucket_shift, int32_t slices,
+                                   int32_t accumulate, float *grad_cbsr, int64_t num_rows,
+                                   int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                                   int32_t dim_k, void *workspace, size_t workspace_bytes,
+                                   void *stream);
+
 /* Pull plan of a CSR graph and its edge values (once per graph, shift and slices):
  * tile_ptr[slices*nb + 1] over tiles t = s*nb + j (rows cut into `slices` slices of
  * ceil(num_rows/slices) <= 65536 rows, nb = maxk_bucket_count(num_cols, shift)); per tile,

@@ -941,15 +941,17 @@ struct PullTile {
     int64_t r0, nrows, c0;
     int s0, s1;
 };
-__device__ __forceinline__ PullTile pull_tile_of(int t, const int32_t *__restrict__ tile_ptr,
+// Tile t = slice * n_buckets + bucket; its entries are [tile_ptr[i], tile_ptr[i + 1]), i = t
+// for a full plan, i = t's position in the tile list for a listed one (pull_q_kernel).
+__device__ __forceinline__ PullTile pull_tile_of(int t, int i, const int32_t *__restrict__ tile_ptr,
                                                  int n_buckets, int rows_per_slice,
                                                  int64_t num_rows, int shift) {
     PullTile p;
     p.r0 = (int64_t)(t / n_buckets) * rows_per_slice;
     p.nrows = num_rows - p.r0 < rows_per_slice ? num_rows - p.r0 : rows_per_slice;
     p.c0 = (int64_t)(t % n_buckets) << shift;
-    p.s0 = tile_ptr[t];
-    p.s1 = tile_ptr[t + 1];
+    p.s0 = tile_ptr[i];
+    p.s1 = tile_ptr[i + 1];
     return p;
 }
 
@@ -1042,15 +1044,19 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
     const float *__restrict__ Gp, const uint8_t *__restrict__ sel_q,
     const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
     float *__restrict__ tile_out, int64_t num_cols, int n_buckets, int n_tiles,
-    int rows_per_slice, int64_t num_rows, int D, int k, int kp, int shift) {
+    int rows_per_slice, int64_t num_rows, int D, int k, int kp, int shift,
+    const int32_t *__restrict__ tile_list) {
+    // tile_list (maxk_sspmm_backward_pull_tiles): only the listed tiles run; tile_ptr then
+    // holds their entry ranges and tile_out their partials, both by list position
     extern __shared__ double acc[];  // [ks << shift], then [kp << shift] selector bytes
     const int tid = threadIdx.x;
     const int ks = pull_ks(kp, shift);
     const int H = k / kp;
     const int tp = MAXK_PULL_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
     if (tp >= n_tiles * H) return;  // the XCD grid's padding
-    const int t = tp / H, h = tp % H;
-    const PullTile p = pull_tile_of(t, tile_ptr, n_buckets, rows_per_slice, num_rows, shift);
+    const int ti = tp / H, h = tp % H;
+    const int t = tile_list ? tile_list[ti] : ti;
+    const PullTile p = pull_tile_of(t, ti, tile_ptr, n_buckets, rows_per_slice, num_rows, shift);
     uint8_t *sel_lds = reinterpret_cast<uint8_t *>(acc + (ks << shift));
     for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
     pull_sel_store(sel_lds, pull_sel_load(sel_q, p.c0, num_cols, k, kp, h, shift), kp, shift);
@@ -1060,16 +1066,22 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
     const auto ers = wave_buffer(ent + p.s0, (uint32_t)(p.s1 - p.s0) * 8u);
     pull_q_entries<LR, U, FULLD, VPL>(acc, sel_lds, grs, ers, p.s1 - p.s0, D, kp, shift);
     __syncthreads();
-    pull_flush(acc, tile_out, t, h, k, kp, shift);
+    pull_flush(acc, tile_out, ti, h, k, kp, shift);
 }
 
 // grad_cbsr rows of bucket j = the sum of its slices' tiles, in slice order.  With lmap
 // (pull_q_kernel's slot order, k % 4 == 0) slot f of row c goes to l = lmap[c * k + f].
+// Listed tiles (bucket_ptr != nullptr, k % 4 == 0): bucket j's tiles are the list positions
+// bucket_tiles[bucket_ptr[j] .. bucket_ptr[j + 1]), in slice order (none: the sum is 0);
+// accumulate adds the sum onto grad_cbsr instead of storing it.
 __global__ __launch_bounds__(kBlock) void pull_reduce_kernel(const float *__restrict__ tile_out,
                                                              const uint8_t *__restrict__ lmap,
                                                              float *__restrict__ grad_cbsr,
                                                              int64_t num_cols, int n_buckets,
-                                                             int slices, int k, int shift) {
+                                                             int slices, int k, int shift,
+                                                             const int32_t *__restrict__ bucket_ptr,
+                                                             const int32_t *__restrict__ bucket_tiles,
+                                                             int accumulate) {
     const int j = blockIdx.x;
     const int64_t c0 = (int64_t)j << shift;
     const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
@@ -1087,18 +1099,36 @@ __global__ __launch_bounds__(kBlock) void pull_reduce_kernel(const float *__rest
         }
         return;
     }
-    float4 a = to[(size_t)j * n4 + i];
-    for (int s = 1; s < slices; ++s) {
-        const float4 b = to[((size_t)s * n_buckets + j) * n4 + i];
-        a.x += b.x;
-        a.y += b.y;
-        a.z += b.z;
-        a.w += b.w;
+    float4 a;
+    if (bucket_ptr) {
+        a = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = bucket_ptr[j]; q < bucket_ptr[j + 1]; ++q) {
+            const float4 b = to[(size_t)bucket_tiles[q] * n4 + i];
+            a.x += b.x;
+            a.y += b.y;
+            a.z += b.z;
+            a.w += b.w;
+        }
+    } else {
+        a = to[(size_t)j * n4 + i];
+        for (int s = 1; s < slices; ++s) {
+            const float4 b = to[((size_t)s * n_buckets + j) * n4 + i];
+            a.x += b.x;
+            a.y += b.y;
+            a.z += b.z;
+            a.w += b.w;
+        }
     }
     if (lmap) {  // four slots of one row (k % 4 == 0) back to their l
         const size_t f0 = (size_t)c0 * k + (size_t)i * 4;
         const uint32_t m = *reinterpret_cast<const uint32_t *>(lmap + f0);
         float *row = grad_cbsr + (f0 / k) * k;
+        if (accumulate) {
+            a.x += row[m & 255u];
+            a.y += row[(m >> 8) & 255u];
+            a.z += row[(m >> 16) & 255u];
+            a.w += row[m >> 24];
+        }
         row[m & 255u] = a.x;
         row[(m >> 8) & 255u] = a.y;
         row[(m >> 16) & 255u] = a.z;
@@ -1470,28 +1500,27 @@ int pull_parts(int k, int shift) {
 }
 }  // namespace maxk
 
-extern "C" size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int64_t num_cols,
-                                                          int32_t dim_origin, int32_t dim_k,
-                                                          int32_t slices) {
-    if (num_rows < 0 || num_cols < 0 || dim_origin <= 0 || dim_k <= 0 || slices <= 0) return 0;
+namespace maxk {
+namespace {
+// Workspace of the pull for `tiles` tile partials: G' (row_div), the partials, slot-ordered
+// selectors and their l map.
+size_t pull_workspace(int64_t num_rows, int64_t num_cols, int32_t dim_origin, int32_t dim_k,
+                      int64_t tiles) {
     // the largest shift any plan may carry bounds the tile partials
     const int shift = std::max(maxk_bucket_shift(dim_k), maxk_pull_shift(dim_k));
-    const int64_t nb = maxk_bucket_count(num_cols, shift);
     const size_t gp = ((size_t)num_rows * dim_origin * sizeof(float) + 255) & ~(size_t)255;
-    const size_t tiles = (size_t)slices * nb * ((size_t)dim_k << shift) * sizeof(float);
+    const size_t tb = (size_t)tiles * ((size_t)dim_k << shift) * sizeof(float);
     // slot-ordered selectors and their l map (pull_sel_kernel), k % 4 == 0
     const size_t selq = dim_k % 4 == 0 ? 2 * (((size_t)num_cols * dim_k + 255) & ~(size_t)255) : 0;
-    return gp + tiles + selq;
+    return gp + tb + selq;
 }
 
-extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
-                                        const uint8_t *cbsr_idx, const int32_t *tile_ptr,
-                                        const uint32_t *ent, int32_t bucket_shift,
-                                        int32_t slices, float *grad_cbsr, int64_t num_rows,
-                                        int64_t num_cols, int64_t num_e, int32_t dim_origin,
-                                        int32_t dim_k, void *workspace, size_t workspace_bytes,
-                                        void *stream) {
-    clear_error();
+int pull_impl(const float *grad_out, const float *row_div, const uint8_t *cbsr_idx,
+              const int32_t *tile_ptr, const uint32_t *ent, int32_t bucket_shift, int32_t slices,
+              bool listed, const int32_t *tile_list, int32_t n_list, const int32_t *bucket_ptr,
+              const int32_t *bucket_tiles, int32_t accumulate, float *grad_cbsr, int64_t num_rows,
+              int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k, void *workspace,
+              size_t workspace_bytes, void *stream) {
     if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, 0)) return rc;
     MAXK_REQUIRE(dim_k % 4 == 0 || dim_k <= 64,
                  "pull backward needs dim_k %% 4 == 0 or dim_k <= 64, got %d", dim_k);
@@ -1517,8 +1546,11 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     MAXK_REQUIRE(grad_cbsr && tile_ptr, "grad_cbsr/tile_ptr must not be NULL");
     MAXK_REQUIRE(num_e == 0 || (grad_out && cbsr_idx && ent),
                  "grad/selector/plan pointers must not be NULL");
-    const size_t need =
-        maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, dim_origin, dim_k, slices);
+    MAXK_REQUIRE(!listed || (parts > 0 && bucket_ptr && n_list >= 0 &&
+                             (n_list == 0 || (tile_list && bucket_tiles))),
+                 "listed tiles need dim_k %% 4 == 0 and tile_list/bucket_ptr/bucket_tiles");
+    const int64_t tiles = listed ? (int64_t)n_list : (int64_t)slices * nb;
+    const size_t need = pull_workspace(num_rows, num_cols, dim_origin, dim_k, tiles);
     MAXK_REQUIRE(workspace && workspace_bytes >= need,
                  "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
     const int k = dim_k;
@@ -1533,7 +1565,6 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
         Gp = reinterpret_cast<const float *>(workspace);
     }
     float *tile_out = reinterpret_cast<float *>(reinterpret_cast<char *>(workspace) + gpb);
-    const unsigned tiles = (unsigned)(slices * nb);
     const size_t acc_b = ((size_t)(k + 1) << bucket_shift) * sizeof(double);
     const size_t sel_b = ((size_t)k << bucket_shift);
     const bool sel_lds = acc_b + sel_b <= kPullLdsBytes;
@@ -1544,7 +1575,7 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     if (parts > 0) {  // quantile-slot form (pull_q_kernel), `parts` workgroups per tile
         const int kp = k / parts;
         const size_t lds_q = ((size_t)pull_ks(kp, bucket_shift) * 8 + kp) << bucket_shift;
-        const size_t tb = (size_t)slices * nb * ((size_t)k << bucket_shift) * sizeof(float);
+        const size_t tb = (size_t)tiles * ((size_t)k << bucket_shift) * sizeof(float);
         const size_t nsel = ((size_t)num_cols * k + 255) & ~(size_t)255;
         uint8_t *sel_q = reinterpret_cast<uint8_t *>(tile_out) + tb;
         uint8_t *lm = sel_q + nsel;
@@ -1555,9 +1586,11 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
         hipLaunchKernelGGL(pull_sel_kernel, dim3((unsigned)ceil_div(num_cols, nd)), dim3(kBlock),
                            0, s, cbsr_idx, sel_q, lm, num_cols, k, kp, vpl);
         MAXK_LAUNCHED("pull_sel_kernel");
-        const int64_t work = (int64_t)tiles * parts;
+        const int64_t work = tiles * parts;
         const bool fulld = dim_origin == kMaxDim;
         const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);
+        lmap = lm;
+        if (work == 0) goto reduce;  // no listed tile: the reduce only permutes / accumulates
         switch (vpl == 2   ? (fulld ? -1 : -2)
                 : vpl == 8 ? (fulld ? -3 : -4)
                            : lanes_per_edge(kp / 4) * 2 + (fulld ? 1 : 0)) {
@@ -1565,7 +1598,8 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
     case CASE:                                                                                \
         hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, FD, VP>), dim3(grid), dim3(1024), \
                            lds_q, s, Gp, sel_q, tile_ptr, ent2, tile_out, num_cols, (int)nb,   \
-                           (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift);   \
+                           (int)tiles, (int)rps, num_rows, dim_origin, k, kp, bucket_shift,    \
+                           tile_list);                                                          \
         break;
 #define MAXK_CASE(LRV) MAXK_CASE_V(LRV * 2 + 1, LRV, true, 4) MAXK_CASE_V(LRV * 2, LRV, false, 4)
             MAXK_CASE(1) MAXK_CASE(2) MAXK_CASE(4) MAXK_CASE(8) MAXK_CASE(16) MAXK_CASE(32)
@@ -1579,16 +1613,15 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
                 return MAXK_ERR_INVALID;
         }
         MAXK_LAUNCHED("pull_q_kernel");
-        lmap = lm;
     } else switch (lanes_per_edge(v4 ? k / 4 : k) * 4 + (sel_lds ? 1 : 0) + (v4 ? 2 : 0)) {
 #define MAXK_CASE(LRV, SL)                                                                    \
     case LRV * 4 + SL + 2:                                                                    \
-        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL, 4>), dim3(tiles), dim3(1024), \
+        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL, 4>), dim3((unsigned)tiles), dim3(1024), \
                            lds, s, Gp, cbsr_idx, tile_ptr, ent2, tile_out, num_cols, (int)nb,  \
                            (int)rps, dim_origin, k, bucket_shift);                            \
         break;                                                                                \
     case LRV * 4 + SL:                                                                        \
-        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL, 1>), dim3(tiles), dim3(1024), \
+        hipLaunchKernelGGL((pull_tile_kernel<LRV, MAXK_PULL_U, SL, 1>), dim3((unsigned)tiles), dim3(1024), \
                            lds, s, Gp, cbsr_idx, tile_ptr, ent2, tile_out, num_cols, (int)nb,  \
                            (int)rps, dim_origin, k, bucket_shift);                            \
         break;
@@ -1605,10 +1638,58 @@ extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_
             return MAXK_ERR_INVALID;
     }
     MAXK_LAUNCHED("pull_tile_kernel");
+reduce:
     hipLaunchKernelGGL(pull_reduce_kernel,
                        dim3((unsigned)nb, (unsigned)ceil_div(ceil_div((int64_t)k << bucket_shift, 4), kBlock)),
                        dim3(kBlock), 0, s, tile_out, lmap, grad_cbsr, num_cols, (int)nb, slices,
-                       k, bucket_shift);
+                       k, bucket_shift, listed ? bucket_ptr : nullptr,
+                       listed ? bucket_tiles : nullptr, accumulate);
     MAXK_LAUNCHED("pull_reduce_kernel");
     return MAXK_OK;
+}
+}  // namespace
+}  // namespace maxk
+
+extern "C" size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                          int32_t dim_origin, int32_t dim_k,
+                                                          int32_t slices) {
+    if (num_rows < 0 || num_cols < 0 || dim_origin <= 0 || dim_k <= 0 || slices <= 0) return 0;
+    const int shift = std::max(maxk_bucket_shift(dim_k), maxk_pull_shift(dim_k));
+    return pull_workspace(num_rows, num_cols, dim_origin, dim_k,
+                          (int64_t)slices * maxk_bucket_count(num_cols, shift));
+}
+
+extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
+                                        const uint8_t *cbsr_idx, const int32_t *tile_ptr,
+                                        const uint32_t *ent, int32_t bucket_shift,
+                                        int32_t slices, float *grad_cbsr, int64_t num_rows,
+                                        int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                                        int32_t dim_k, void *workspace, size_t workspace_bytes,
+                                        void *stream) {
+    clear_error();
+    return pull_impl(grad_out, row_div, cbsr_idx, tile_ptr, ent, bucket_shift, slices, false,
+                     nullptr, 0, nullptr, nullptr, 0, grad_cbsr, num_rows, num_cols, num_e, dim_origin, dim_k,
+                     workspace, workspace_bytes, stream);
+}
+
+extern "C" size_t maxk_sspmm_backward_pull_tiles_workspace_size(int64_t num_rows,
+                                                                int64_t num_cols,
+                                                                int32_t dim_origin,
+                                                                int32_t dim_k, int32_t n_tiles) {
+    if (num_rows < 0 || num_cols < 0 || dim_origin <= 0 || dim_k <= 0 || n_tiles < 0) return 0;
+    return pull_workspace(num_rows, num_cols, dim_origin, dim_k, n_tiles);
+}
+
+extern "C" int maxk_sspmm_backward_pull_tiles(
+    const float *grad_out, const float *row_div, const uint8_t *cbsr_idx,
+    const int32_t *tile_list, const int32_t *tile_ent, int32_t n_tiles,
+    const int32_t *bucket_ptr, const int32_t *bucket_tiles, const uint32_t *ent,
+    int32_t bucket_shift, int32_t slices, int32_t accumulate, float *grad_cbsr,
+    int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
+    void *workspace, size_t workspace_bytes, void *stream) {
+    clear_error();
+    MAXK_REQUIRE(tile_ent, "tile_ent must not be NULL");
+    return pull_impl(grad_out, row_div, cbsr_idx, tile_ent, ent, bucket_shift, slices, true,
+                     tile_list, n_tiles, bucket_ptr, bucket_tiles, accumulate, grad_cbsr, num_rows, num_cols,
+                     num_e, dim_origin, dim_k, workspace, workspace_bytes, stream);
 }

@@ -362,7 +362,76 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     return plan
 
 
-BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic")
+_HYBRID_CACHE: "dict" = {}
+
+
+def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                num_cols: int, k: int, dim: int = 256, density: float = 0.5,
+                cache: bool = True):
+    """Plan of the "hybrid" backward: the pull over the dense tiles of the graph's pull plan
+    (at least `density` entries per row of the tile's slice), the two-phase csc over the other
+    edges.  A community-ordered graph keeps most edges in the tiles near the diagonal, which
+    pull well, while a pull over every tile would write one [num_cols, k] partial per row
+    slice (maxk_sspmm_backward_pull_tiles in include/maxk_hip.h).  Returns (tile_list,
+    tile_ent, bucket_ptr, bucket_tiles, ent, shift, S, (off_indptr, off_indices, off_values,
+    off_transpose_plan)); cached like pull_plan.  k % 4 == 0."""
+    if k % 4:
+        raise RuntimeError(f"hybrid backward needs k % 4 == 0, got k={k}")
+    key = (id(indptr), id(indices), id(values), int(k), int(dim), float(density))
+    hit = _HYBRID_CACHE.get(key)
+    if cache and hit is not None:
+        rp, ri, rv, nc, pv, vi, vv, plan = hit
+        if (rp() is indptr and ri() is indices and rv() is values and nc == num_cols
+                and pv == indptr._version and vi == indices._version
+                and vv == values._version):
+            return plan
+    tptr, ent, shift, S = pull_plan(indptr, indices, values, num_cols, k, dim, cache=False)
+    dev = indices.device
+    num_rows = indptr.numel() - 1
+    nb = int(_lib().maxk_bucket_count(num_cols, shift))
+    rps = -(-num_rows // S)
+    cnt = torch.diff(tptr.long())
+    t_all = torch.arange(S * nb, device=dev)
+    rows_in = torch.clamp(num_rows - (t_all // nb) * rps, max=rps).clamp(min=1)
+    dense = (cnt > 0) & (cnt >= density * rows_in)
+    t_of = torch.repeat_interleave(t_all, cnt)
+    keep = dense[t_of]
+    tile_list = torch.nonzero(dense).flatten()
+    tile_ent = torch.zeros(tile_list.numel() + 1, dtype=torch.int64, device=dev)
+    tile_ent[1:] = torch.cumsum(cnt[tile_list], 0)
+    j = tile_list % nb
+    order = torch.argsort(j * S + tile_list // nb)
+    bucket_ptr = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+    bucket_ptr[1:] = torch.cumsum(torch.bincount(j, minlength=nb), 0)
+    ent_d = ent[keep].contiguous()
+    # the other edges back to a CSR (rows, then columns), with their weights
+    eo = ent[~keep]
+    to = t_of[~keep]
+    x = eo[:, 0].long() & 0xffffffff
+    rows = (to // nb) * rps + (x & 0xffff)
+    cols = ((to % nb) << shift) + (x >> 16)
+    vals = eo[:, 1].contiguous().view(torch.float32)
+    srt = torch.argsort(rows * num_cols + cols)
+    off_ip = torch.zeros(num_rows + 1, dtype=torch.int64, device=dev)
+    off_ip[1:] = torch.cumsum(torch.bincount(rows, minlength=num_rows), 0)
+    off_ix = cols[srt].to(torch.int32).contiguous()
+    off_val = vals[srt].contiguous()
+    off_ip = off_ip.to(torch.int32)
+    off = (off_ip, off_ix, off_val, transpose_plan(off_ix, num_cols, cache=False))
+    i32 = lambda t: t.to(torch.int32).contiguous()  # noqa: E731
+    plan = (i32(tile_list), i32(tile_ent), i32(bucket_ptr), i32(order), ent_d, shift, S, off)
+    del tptr, ent, cnt, t_all, rows_in, t_of, keep, eo, to, x, rows, cols, vals, srt
+    if cache:
+        if key not in _HYBRID_CACHE:
+            for t in (indptr, indices, values):
+                weakref.finalize(t, _HYBRID_CACHE.pop, key, None)
+        _HYBRID_CACHE[key] = (weakref.ref(indptr), weakref.ref(indices), weakref.ref(values),
+                              int(num_cols), indptr._version, indices._version, values._version,
+                              plan)
+    return plan
+
+
+BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid")
 
 
 _LOCALITY: "dict" = {}
@@ -434,6 +503,9 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
         raise RuntimeError(f"backward mode 'pull' needs k % 4 == 0 or k <= 64, got k={k}")
     if mode == "pull" and dim is not None and dim % 4 != 0:
         raise RuntimeError(f"backward mode 'pull' needs dim_origin % 4 == 0, got {dim}")
+    if mode == "hybrid" and (k % 4 != 0 or (dim is not None and dim % 4 != 0)):
+        raise RuntimeError(f"backward mode 'hybrid' needs k % 4 == 0 and dim_origin % 4 == 0, "
+                           f"got k={k}, dim={dim}")
     return mode
 
 
@@ -444,9 +516,11 @@ def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[s
     num_rows (default num_cols) and dim only steer mode "auto".  Mode "pull" also needs
     the graph's indptr and edge values."""
     mode = _bwd_mode(mode, k, indices.numel(), num_cols, num_rows, dim)
-    if mode == "pull":
+    if mode in ("pull", "hybrid"):
         if indptr is None or values is None:
-            raise RuntimeError("backward_plan: mode 'pull' needs indptr= and values=")
+            raise RuntimeError(f"backward_plan: mode '{mode}' needs indptr= and values=")
+        if mode == "hybrid":
+            return hybrid_plan(indptr, indices, values, num_cols, k, dim or 256)
         return pull_plan(indptr, indices, values, num_cols, k, dim or 256)
     if mode == "bucket":
         return bucket_plan(indices, num_cols, k)
@@ -472,7 +546,10 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     the graph's bucket plan (built once and cached, or `plan=` from bucket_plan()).
     mode "csc": two-phase, atomic-free and bitwise deterministic, using the graph's
     transpose plan (built once and cached, or `plan=` from transpose_plan()).
-    mode "atomic": one global fp32 atomic per (edge, l); no preprocessing."""
+    mode "atomic": one global fp32 atomic per (edge, l); no preprocessing.
+    mode "hybrid" (k % 4 == 0; chosen explicitly, never by "auto"): the pull over the dense
+    tiles of the pull plan and csc over the other edges (hybrid_plan), for large graphs whose
+    vertex order groups their communities."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32), (grad_output, "grad_output", torch.float32),
                      (cbsr_idx, "sparse_selector", torch.uint8)):
@@ -497,6 +574,25 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     L = _lib()
     E = indices.numel()
     mode = _bwd_mode(mode, k, E, num_cols, num_rows, D)
+    if mode == "hybrid":
+        tl, te, bp, bt, ent, shift, S, off = (plan if plan is not None else
+                                             hybrid_plan(indptr, indices, values, num_cols, k, D))
+        oip, oix, oval, otp = off
+        if oix.numel():  # the sparse tiles' edges: two-phase csc, into out
+            sspmm_backward(oip, oix, oval, grad_output, cbsr_idx, row_div=row_div, chunk=chunk,
+                           out=out, validate=False, mode="csc", plan=otp)
+        else:
+            out.zero_()
+        n_t = tl.numel()
+        ws_bytes = L.maxk_sspmm_backward_pull_tiles_workspace_size(num_rows, num_cols, D, k, n_t)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            _capi.check(L.maxk_sspmm_backward_pull_tiles(
+                _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tl), _ptr(te), n_t,
+                _ptr(bp), _ptr(bt), _ptr(ent), shift, S, 1, _ptr(out), num_rows, num_cols,
+                ent.shape[0], D, k, _ptr(ws), ws.numel(), _stream(dev)),
+                "maxk_sspmm_backward_pull_tiles")
+        return out
     if mode == "pull":
         tptr, ent, shift, S = (plan if plan is not None else
                                pull_plan(indptr, indices, values, num_cols, k, D))

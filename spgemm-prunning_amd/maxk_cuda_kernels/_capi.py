@@ -51,6 +51,10 @@ SIGNATURES = {
     "maxk_sspmm_backward_pull_workspace_size": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward_pull": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _p, _i64, _i64,
                                                 _i64, _i32, _i32, _p, _sz, _p]),
+    "maxk_sspmm_backward_pull_tiles_workspace_size": (_sz, [_i64, _i64, _i32, _i32, _i32]),
+    "maxk_sspmm_backward_pull_tiles": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _p, _p, _p, _i32,
+                                                      _i32, _i32, _p, _i64, _i64, _i64, _i32,
+                                                      _i32, _p, _sz, _p]),
     "maxk_pull_shift": (ctypes.c_int, [_i32]),
     "maxk_pull_slices": (ctypes.c_int, [_i64, _i32, _i32]),
     "maxk_pull_plan_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32]),

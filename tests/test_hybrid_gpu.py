@@ -1,0 +1,49 @@
+"""GPU parity of the "hybrid" backward (the pull over a plan's dense tiles through
+maxk_sspmm_backward_pull_tiles, accumulating onto the two-phase csc of the other edges)
+against the oracle: on a community-ordered graph and a randomly labelled one, at tile
+densities that send every tile, none and part of them to the pull.  Tolerance as in
+test_parity_gpu."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from test_parity_gpu import close
+
+pytestmark = pytest.mark.gpu
+
+
+def _graphs(cuda):
+    import maxk_graph
+    V, E = 6000, 6000 + 2 * 120000
+    ip, ix = maxk_graph.community_graph(V, E, 0.75, 30, 12, 0.9, 5, torch.device(cuda))
+    ip2, ix2, _ = maxk_graph.permute_graph(ip, ix, maxk_graph.locality_order(ip, ix))
+    return {"random": (ip, ix), "ordered": (ip2, ix2)}
+
+
+@pytest.mark.parametrize("k", [8, 16, 32])
+@pytest.mark.parametrize("density", [0.0, 0.3, 1e9])
+@pytest.mark.parametrize("name", ["random", "ordered"])
+def test_hybrid_against_oracle(cuda, name, density, k):
+    import maxk_cuda_kernels as mk
+    ip, ix = _graphs(cuda)[name]
+    V, D = ip.numel() - 1, 256
+    rng = np.random.default_rng(k)
+    val = torch.rand(ix.numel(), device=cuda)
+    x = rng.standard_normal((V, D), dtype=np.float32)
+    cv, ci = O.topk(x, k)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    div = torch.clamp(torch.diff(ip).float(), min=1.0)
+    plan = mk.hybrid_plan(ip, ix, val, V, k, D, density=density)
+    tl, _, _, _, ent_d, _, _, off = plan
+    if density == 0.0:
+        assert off[1].numel() == 0  # every non-empty tile pulls
+    if density == 1e9:
+        assert tl.numel() == 0 and ent_d.shape[0] == 0  # everything through csc
+    assert ent_d.shape[0] + off[1].numel() == ix.numel()
+    ci_t = torch.from_numpy(ci).to(cuda)
+    gs = mk.sspmm_backward(ip, ix, val, torch.from_numpy(g).to(cuda), ci_t, row_div=div,
+                           mode="hybrid", plan=plan)
+    go = O.sspmm_bwd(ip.cpu().numpy(), ix.cpu().numpy(), val.cpu().numpy(), g, ci,
+                     row_div=div.cpu().numpy())
+    close(gs, go)

@@ -8,6 +8,8 @@ run random
 run random_pull --bwd-mode pull --no-rocsparse
 run ordered --reorder
 run ordered_csc --reorder --bwd-mode csc --no-rocsparse
+run ordered_hybrid --reorder --bwd-mode hybrid --no-rocsparse
+run random_hybrid --bwd-mode hybrid --no-rocsparse
 timeout -k 10 300 python tools/halo_bytes.py --graph products_comm --device cuda > $O/halo_random.txt 2>&1
 timeout -k 10 300 python tools/halo_bytes.py --graph products_comm --device cuda --reorder > $O/halo_ordered.txt 2>&1
 cat $O/halo_random.txt $O/halo_ordered.txt
