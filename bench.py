@@ -366,7 +366,8 @@ def main():
     # one validated call (row_ptr/col_idx/selector ranges) before the raw timed launches
     mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, validate=True)
     # per-graph setup (like the reference's warp4 files): the backward's bucket / transpose plan
-    args.bwd_mode = mk._bwd_mode(args.bwd_mode, k, El, n_cols, nl, D)  # "auto" -> the mode that runs
+    # "auto" -> the mode that runs
+    args.bwd_mode = mk._bwd_mode(args.bwd_mode, k, El, n_cols, nl, D, (l_row_ptr, l_col))
     torch.cuda.synchronize()
     t_plan = time.perf_counter()
     plan = mk.backward_plan(l_col, n_cols, k, args.bwd_mode, indptr=l_row_ptr, values=l_val, dim=D)

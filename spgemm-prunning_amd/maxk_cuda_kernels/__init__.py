@@ -363,10 +363,15 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
 
 
 _HYBRID_CACHE: "dict" = {}
+# a tile pulls when it holds at least this many entries per row of its slice
+HYBRID_DENSITY = 0.5
+# mode "auto" picks "hybrid" on a sparse graph whose pull_locality reaches this (products-
+# sized, k=32: 1.02 (random labels) csc 8.2 vs hybrid 8.4 ms; 1.9: 8.1 vs 6.4; 6.9: 7.4 vs 4.7)
+HYBRID_LOCALITY = 1.5
 
 
 def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
-                num_cols: int, k: int, dim: int = 256, density: float = 0.5,
+                num_cols: int, k: int, dim: int = 256, density: Optional[float] = None,
                 cache: bool = True):
     """Plan of the "hybrid" backward: the pull over the dense tiles of the graph's pull plan
     (at least `density` entries per row of the tile's slice), the two-phase csc over the other
@@ -374,7 +379,10 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
     pull well, while a pull over every tile would write one [num_cols, k] partial per row
     slice (maxk_sspmm_backward_pull_tiles in include/maxk_hip.h).  Returns (tile_list,
     tile_ent, bucket_ptr, bucket_tiles, ent, shift, S, (off_indptr, off_indices, off_values,
-    off_transpose_plan)); cached like pull_plan.  k % 4 == 0."""
+    off_transpose_plan)); cached like pull_plan.  k % 4 == 0.  `density` defaults to
+    MAXK_HYBRID_DENSITY or HYBRID_DENSITY."""
+    if density is None:
+        density = float(os.environ.get("MAXK_HYBRID_DENSITY", HYBRID_DENSITY))
     if k % 4:
         raise RuntimeError(f"hybrid backward needs k % 4 == 0, got k={k}")
     key = (id(indptr), id(indices), id(values), int(k), int(dim), float(density))
@@ -444,7 +452,7 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
     vertex order groups its communities (maxk_graph.locality_order) has many more, whatever
     the average.  One pass over the edges (columns sorted within rows, else an under-
     estimate), cached per (indptr, indices, shift) and their versions.  Reported by bench.py
-    (extra.pull_locality); it does not steer mode "auto" (see _bwd_mode)."""
+    (extra.pull_locality); on sparse graphs it steers mode "auto" to "hybrid" (_bwd_mode)."""
     key = (id(indptr), id(indices), int(shift))
     hit = _LOCALITY.get(key)
     if hit is not None:
@@ -471,7 +479,8 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
 
 
 def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0,
-              num_rows: Optional[int] = None, dim: Optional[int] = None) -> str:
+              num_rows: Optional[int] = None, dim: Optional[int] = None,
+              graph: Optional[tuple] = None) -> str:
     """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) picks "pull"
     where it measured faster than "csc": k % 4 == 0 or k <= 64, dim % 4 == 0 when dim is
     given, and at
@@ -479,9 +488,11 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
     (Reddit k=16: 2.2, k=64: 0.54; ogbn-proteins k=64: 1.2; ogbn-products: 0.02), or a
     gradient G of at most 64 MiB (num_rows x dim x 4 B; Flickr: 23 MB, 0.05 vs 0.13 ms), which
     stays cache-resident however sparse the graph; for more than 256 x 65536 rows "bucket"
-    (k <= 16) stands in.  Locality (pull_locality) does not enter: where the average is
-    sparse the pull's per-slice partials ([num_cols, k] per row slice) already outweigh it
-    (a community-ordered ogbn-products-sized graph: 46 ms against 8 ms csc).
+    (k <= 16) stands in.  On a sparse graph the whole pull loses even with locality (its
+    per-slice partials, [num_cols, k] per row slice: a community-ordered ogbn-products-sized
+    graph 46 ms against 8 ms csc), but where `graph` = (indptr, indices) is
+    given and its pull_locality reaches HYBRID_LOCALITY (k % 4 == 0, dim % 4 == 0) "hybrid"
+    pulls the dense tiles and runs csc over the rest (that graph: 4.7 against 7.4 ms).
     "bucket" (two-phase with the same fp64 accumulator) stays selectable."""
     mode = mode or os.environ.get("MAXK_BWD_MODE", "auto")
     if mode not in BWD_MODES:
@@ -497,6 +508,10 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
                 mode = "pull"
             elif dense and k <= 16 and k % 4 == 0:
                 mode = "bucket"
+            elif (graph is not None and k % 4 == 0 and rows <= 256 * 65536 and num_e > 0
+                  and pull_locality(graph[0], graph[1], int(_lib().maxk_pull_shift(int(k))))
+                  >= HYBRID_LOCALITY):
+                mode = "hybrid"
     if mode == "bucket" and k % 4 != 0:
         raise RuntimeError(f"backward mode 'bucket' needs k % 4 == 0, got k={k}")
     if mode == "pull" and k % 4 != 0 and k > 64:
@@ -515,7 +530,8 @@ def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[s
     """The per-graph plan sspmm_backward needs for `mode` at width k (None for "atomic");
     num_rows (default num_cols) and dim only steer mode "auto".  Mode "pull" also needs
     the graph's indptr and edge values."""
-    mode = _bwd_mode(mode, k, indices.numel(), num_cols, num_rows, dim)
+    mode = _bwd_mode(mode, k, indices.numel(), num_cols, num_rows, dim,
+                     None if indptr is None else (indptr, indices))
     if mode in ("pull", "hybrid"):
         if indptr is None or values is None:
             raise RuntimeError(f"backward_plan: mode '{mode}' needs indptr= and values=")
@@ -547,7 +563,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     mode "csc": two-phase, atomic-free and bitwise deterministic, using the graph's
     transpose plan (built once and cached, or `plan=` from transpose_plan()).
     mode "atomic": one global fp32 atomic per (edge, l); no preprocessing.
-    mode "hybrid" (k % 4 == 0; chosen explicitly, never by "auto"): the pull over the dense
+    mode "hybrid" (k % 4 == 0; "auto" picks it on sparse graphs with locality): the pull over the dense
     tiles of the pull plan and csc over the other edges (hybrid_plan), for large graphs whose
     vertex order groups their communities."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
@@ -573,7 +589,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             raise RuntimeError("out must be [num_cols, k]")
     L = _lib()
     E = indices.numel()
-    mode = _bwd_mode(mode, k, E, num_cols, num_rows, D)
+    mode = _bwd_mode(mode, k, E, num_cols, num_rows, D, (indptr, indices))
     if mode == "hybrid":
         tl, te, bp, bt, ent, shift, S, off = (plan if plan is not None else
                                              hybrid_plan(indptr, indices, values, num_cols, k, D))

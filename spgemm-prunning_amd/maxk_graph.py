@@ -147,6 +147,10 @@ PRESETS = {
     # 90 % of the edges inside one), randomly labelled: the locality a real graph has, hidden
     "products_comm": dict(V=2_449_029, E=123_718_280, alpha=0.75, i0=3000, D=256, k=32,
                           communities=2_000, p_in=0.9),
+    # the same with half of the edges inside a community: a weaker locality, to place the
+    # hybrid backward's switch-over (maxk_cuda_kernels._bwd_mode)
+    "products_comm_p50": dict(V=2_449_029, E=123_718_280, alpha=0.75, i0=3000, D=256, k=32,
+                              communities=2_000, p_in=0.5),
     "proteins": dict(V=132_534, E=79_122_504, alpha=0.45, i0=2000, D=256, k=64),
     "flickr": dict(V=89_250, E=989_006, alpha=0.9, i0=30, D=64, k=16),
 }

@@ -154,7 +154,8 @@ def main(argv=None):
         print(f"{tag} maxk_backward {t_b:.4f}")
         print(f"# {tag} check maxk vs library SpMM: max rel err {err:.3e} "
               f"({'PASS' if err < 1e-3 else 'FAIL'})", file=sys.stderr)
-        results.append({"k": k, "bwd_mode": mk._bwd_mode(args.bwd_mode, k, E, V, V, D),
+        results.append({"k": k, "bwd_mode": mk._bwd_mode(args.bwd_mode, k, E, V, V, D,
+                                                         (row_ptr, col)),
                         "maxk_ms": t_f, "maxk_backward_ms": t_b, "max_rel_err": err,
                         "speedup_fwd": t_lib / t_f, "speedup_bwd": t_lib / t_b,
                         "speedup_fwd_vs_best": t_best / t_f, "speedup_bwd_vs_best": t_best / t_b,

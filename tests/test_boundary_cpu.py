@@ -141,6 +141,19 @@ def test_backward_mode_resolution():
     assert mk._bwd_mode("auto", 64, **proteins) == "pull"
     assert mk._bwd_mode("auto", 32, **products) == "csc"
     assert mk._bwd_mode("auto", 16, **products, dim=256) == "csc"
+    # a sparse graph whose vertex order groups its neighbours (pull_locality >= 1.5): "hybrid";
+    # randomly labelled: csc (the locality is read off the CSR, sizes from the keywords)
+    V, deg = 1 << 20, 8
+    rows = torch.arange(V).repeat_interleave(deg)
+    band = (rows + torch.arange(deg).repeat(V)) % V
+    ip = torch.arange(0, V * deg + 1, deg, dtype=torch.int32)
+    ix_band = torch.sort(band.view(V, deg), 1).values.flatten().to(torch.int32)
+    ix_rand = torch.sort(torch.randint(0, V, (V, deg), generator=torch.Generator().manual_seed(0)),
+                         1).values.flatten().to(torch.int32)
+    assert mk._bwd_mode("auto", 32, **products, dim=256, graph=(ip, ix_band)) == "hybrid"
+    assert mk._bwd_mode("auto", 32, **products, dim=256, graph=(ip, ix_rand)) == "csc"
+    assert mk._bwd_mode("auto", 30, **products, dim=256, graph=(ip, ix_band)) == "csc"
+    assert mk._bwd_mode("auto", 16, **reddit, dim=256, graph=(ip, ix_rand)) == "pull"
     # a small gradient (Flickr, 23 MB) stays cache-resident: pull however sparse the graph
     flickr = dict(num_e=989_006, num_cols=89_250, num_rows=89_250)
     assert mk._bwd_mode("auto", 16, **flickr) == "csc"
