@@ -185,10 +185,16 @@ int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
  * diagonal) and the rest of the edges go through the two-phase backward (the "hybrid" mode
  * of the Python binding).  tile_list[n_tiles]: tile ids t = s*nb + j, increasing;
  * tile_ent[n_tiles + 1]: their entry ranges in ent; bucket_ptr[nb + 1] / bucket_tiles[n_tiles]:
- * per bucket, the positions in tile_list of its tiles in slice order.  accumulate != 0 adds
- * the result onto grad_cbsr (which then holds the other edges' sum), else stores it.  The
+ * per bucket, the positions in tile_list of its tiles in slice order.  accumulate bit 0 adds
+ * the result onto grad_cbsr (which then holds the other edges' sum), else stores it;
+ * MAXK_PULL_NO_REDUCE stops once the tile partials are in the workspace and
+ * MAXK_PULL_REDUCE_ONLY, with otherwise the same arguments and workspace, runs only the
+ * reduce onto grad_cbsr, so the tile kernels can run on another stream beside the two-phase
+ * form of the other edges, joined before the reduce.  The
  * workspace holds n_tiles tile partials: maxk_sspmm_backward_pull_tiles_workspace_size.
  * Replaces the same reference kernels as maxk_sspmm_backward (spmm_maxk_backward.cu:15-121). */
+#define MAXK_PULL_NO_REDUCE 2
+#define MAXK_PULL_REDUCE_ONLY 4
 size_t maxk_sspmm_backward_pull_tiles_workspace_size(int64_t num_rows, int64_t num_cols,
                                                      int32_t dim_origin, int32_t dim_k,
                                                      int32_t n_tiles);

@@ -1553,10 +1553,17 @@ int pull_impl(const float *grad_out, const float *row_div, const uint8_t *cbsr_i
     const size_t need = pull_workspace(num_rows, num_cols, dim_origin, dim_k, tiles);
     MAXK_REQUIRE(workspace && workspace_bytes >= need,
                  "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
+    // accumulate: bit 0 adds onto grad_cbsr; bit 1 (MAXK_PULL_NO_REDUCE) stops at the tile
+    // partials, bit 2 (MAXK_PULL_REDUCE_ONLY) runs only the reduce over a workspace the same
+    // call with bit 1 filled (listed tiles only: the hybrid runs the two-phase form between)
+    const bool front = !(accumulate & MAXK_PULL_REDUCE_ONLY);
+    const bool back = !(accumulate & MAXK_PULL_NO_REDUCE);
+    MAXK_REQUIRE(listed || (front && back), "reduce-only / no-reduce need listed tiles");
+    MAXK_REQUIRE(front || back, "no-reduce and reduce-only together run nothing");
     const int k = dim_k;
     const float *Gp = grad_out;
     const size_t gpb = ((size_t)num_rows * dim_origin * sizeof(float) + 255) & ~(size_t)255;
-    if (row_div && num_rows > 0 && num_e > 0) {
+    if (front && row_div && num_rows > 0 && num_e > 0) {
         const int64_t n4 = num_rows * dim_origin / 4;
         hipLaunchKernelGGL(gprime_kernel, dim3((unsigned)ceil_div(n4, kBlock)), dim3(kBlock), 0,
                            s, grad_out, row_div, reinterpret_cast<float *>(workspace), n4,
@@ -1583,13 +1590,14 @@ int pull_impl(const float *grad_out, const float *row_div, const uint8_t *cbsr_i
         // values per lane: 4 (one u32 selector word per lane; 2 lanes per entry for 8-slot
         // parts), 8 for k = 8 (one lane per entry, one u64 selector word; MAXK_PULL_VPL8)
         const int vpl = kp != 8 ? 4 : MAXK_PULL_VPL8 ? MAXK_PULL_VPL8 : parts == 1 ? 8 : 4;
+        lmap = lm;
+        if (!front) goto reduce;
         hipLaunchKernelGGL(pull_sel_kernel, dim3((unsigned)ceil_div(num_cols, nd)), dim3(kBlock),
                            0, s, cbsr_idx, sel_q, lm, num_cols, k, kp, vpl);
         MAXK_LAUNCHED("pull_sel_kernel");
         const int64_t work = tiles * parts;
         const bool fulld = dim_origin == kMaxDim;
         const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);
-        lmap = lm;
         if (work == 0) goto reduce;  // no listed tile: the reduce only permutes / accumulates
         switch (vpl == 2   ? (fulld ? -1 : -2)
                 : vpl == 8 ? (fulld ? -3 : -4)
@@ -1639,11 +1647,12 @@ int pull_impl(const float *grad_out, const float *row_div, const uint8_t *cbsr_i
     }
     MAXK_LAUNCHED("pull_tile_kernel");
 reduce:
+    if (!back) return MAXK_OK;
     hipLaunchKernelGGL(pull_reduce_kernel,
                        dim3((unsigned)nb, (unsigned)ceil_div(ceil_div((int64_t)k << bucket_shift, 4), kBlock)),
                        dim3(kBlock), 0, s, tile_out, lmap, grad_cbsr, num_cols, (int)nb, slices,
                        k, bucket_shift, listed ? bucket_ptr : nullptr,
-                       listed ? bucket_tiles : nullptr, accumulate);
+                       listed ? bucket_tiles : nullptr, accumulate & 1);
     MAXK_LAUNCHED("pull_reduce_kernel");
     return MAXK_OK;
 }

@@ -363,6 +363,16 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
 
 
 _HYBRID_CACHE: "dict" = {}
+MAXK_PULL_NO_REDUCE, MAXK_PULL_REDUCE_ONLY = 2, 4  # include/maxk_hip.h
+_SIDE: "dict" = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """One extra HIP stream per device (the hybrid backward's tile kernels)."""
+    i = dev.index if dev.index is not None else torch.cuda.current_device()
+    if i not in _SIDE:
+        _SIDE[i] = torch.cuda.Stream(device=i)
+    return _SIDE[i]
 # a tile pulls when it holds at least this many entries per row of its slice
 HYBRID_DENSITY = 0.5
 # mode "auto" picks "hybrid" on a sparse graph whose pull_locality reaches this (products-
@@ -594,20 +604,35 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         tl, te, bp, bt, ent, shift, S, off = (plan if plan is not None else
                                              hybrid_plan(indptr, indices, values, num_cols, k, D))
         oip, oix, oval, otp = off
-        if oix.numel():  # the sparse tiles' edges: two-phase csc, into out
-            sspmm_backward(oip, oix, oval, grad_output, cbsr_idx, row_div=row_div, chunk=chunk,
-                           out=out, validate=False, mode="csc", plan=otp)
-        else:
-            out.zero_()
         n_t = tl.numel()
         ws_bytes = L.maxk_sspmm_backward_pull_tiles_workspace_size(num_rows, num_cols, D, k, n_t)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        with torch.cuda.device(dev):
+
+        def tiles(flags):
             _capi.check(L.maxk_sspmm_backward_pull_tiles(
                 _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tl), _ptr(te), n_t,
-                _ptr(bp), _ptr(bt), _ptr(ent), shift, S, 1, _ptr(out), num_rows, num_cols,
+                _ptr(bp), _ptr(bt), _ptr(ent), shift, S, flags, _ptr(out), num_rows, num_cols,
                 ent.shape[0], D, k, _ptr(ws), ws.numel(), _stream(dev)),
                 "maxk_sspmm_backward_pull_tiles")
+        with torch.cuda.device(dev):
+            overlap = (oix.numel() > 0 and n_t > 0
+                       and os.environ.get("MAXK_HYBRID_STREAMS", "1") != "0")
+            if overlap:  # the tile kernels on a side stream beside the csc, joined at the reduce
+                main = torch.cuda.current_stream(dev)
+                side = _side_stream(dev)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    tiles(MAXK_PULL_NO_REDUCE)
+            if oix.numel():  # the sparse tiles' edges: two-phase csc, into out
+                sspmm_backward(oip, oix, oval, grad_output, cbsr_idx, row_div=row_div,
+                               chunk=chunk, out=out, validate=False, mode="csc", plan=otp)
+            else:
+                out.zero_()
+            if overlap:
+                main.wait_stream(side)
+                tiles(MAXK_PULL_REDUCE_ONLY | 1)
+            else:
+                tiles(1)
         return out
     if mode == "pull":
         tptr, ent, shift, S = (plan if plan is not None else

@@ -34,7 +34,8 @@ import maxk_graph  # noqa: E402
 import maxk_layers  # noqa: E402
 
 # (input feature dim, classes) of the published datasets (ogbn-products: 100 / 47)
-DATASET_SHAPES = {"products": (100, 47), "reddit": (602, 41), "proteins": (8, 112),
+DATASET_SHAPES = {"products": (100, 47), "products_comm": (100, 47), "reddit": (602, 41),
+                  "proteins": (8, 112),
                   "flickr": (500, 7)}
 
 
@@ -123,6 +124,9 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--graph-dir", default=None)
     ap.add_argument("--no-library", action="store_true")
+    ap.add_argument("--reorder", action="store_true",
+                    help="relabel the graph by maxk_graph.locality_order first (untimed, once "
+                         "per graph; features and labels are synthetic, so none to permute)")
     args = ap.parse_args(argv)
     if not torch.cuda.is_available():
         raise SystemExit("maxk_train_bench needs an MI355X (HIP device)")
@@ -135,6 +139,14 @@ def main(argv=None):
     else:
         indptr, indices = maxk_graph.synthetic_graph(args.graph, device=dev)
         source = "synthetic"
+    t_reorder = None
+    if args.reorder:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        indptr, indices, _ = maxk_graph.permute_graph(
+            indptr, indices, maxk_graph.locality_order(indptr, indices))
+        torch.cuda.synchronize()
+        t_reorder = round(time.perf_counter() - t0, 3)
     g = maxk_layers.CSRGraph(indptr, indices)  # SAGE: unit edge weights, mean by in-degree
     V = g.num_nodes
     f_in, n_cls = DATASET_SHAPES.get(args.graph, (128, 16))
@@ -149,6 +161,8 @@ def main(argv=None):
     out = {"graph": args.graph, "source": source, "V": V, "E": indices.numel(),
            "hidden": args.hidden, "k": args.k, "layers": args.layers, "epochs": args.epochs,
            "maxk_epoch_ms": round(ms, 3), "first_loss": loss0}
+    if args.reorder:
+        out["reorder_s"] = t_reorder
     if not args.no_library:
         ms_lib, loss_lib = time_epochs(ref, LibraryGraph(g), x, y, args.epochs, args.warmup)
         out.update({"library_epoch_ms": round(ms_lib, 3), "speedup": round(ms_lib / ms, 3),

@@ -1,6 +1,7 @@
 """GPU parity of the "hybrid" backward (the pull over a plan's dense tiles through
 maxk_sspmm_backward_pull_tiles, accumulating onto the two-phase csc of the other edges)
-against the oracle: on a community-ordered graph and a randomly labelled one, at tile
+against the oracle, with the tile kernels beside the csc on a side stream or in line: on a
+community-ordered graph and a randomly labelled one, at tile
 densities that send every tile, none and part of them to the pull.  Tolerance as in
 test_parity_gpu."""
 import numpy as np
@@ -21,11 +22,15 @@ def _graphs(cuda):
     return {"random": (ip, ix), "ordered": (ip2, ix2)}
 
 
+@pytest.mark.parametrize("streams", ["1", "0"])
 @pytest.mark.parametrize("k", [8, 16, 32])
 @pytest.mark.parametrize("density", [0.0, 0.3, 1e9])
 @pytest.mark.parametrize("name", ["random", "ordered"])
-def test_hybrid_against_oracle(cuda, name, density, k):
+def test_hybrid_against_oracle(cuda, name, density, k, streams, monkeypatch):
+    """streams "1": the tile kernels on a side stream beside the csc (the default), "0": in
+    line after it."""
     import maxk_cuda_kernels as mk
+    monkeypatch.setenv("MAXK_HYBRID_STREAMS", streams)
     ip, ix = _graphs(cuda)[name]
     V, D = ip.numel() - 1, 256
     rng = np.random.default_rng(k)
