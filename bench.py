@@ -471,6 +471,9 @@ def main():
     # edges per occupied (source row, pull bucket): the locality the pull backward feeds on
     extra["pull_locality"] = round(
         mk.pull_locality(l_row_ptr, l_col, int(mk._lib().maxk_pull_shift(k))), 3)
+    if args.bwd_mode == "hybrid":  # share of the edges the pulled tiles hold, and their count
+        extra["hybrid_pull_edges_frac"] = round(plan[4].shape[0] / max(1, El), 4)
+        extra["hybrid_pull_tiles"] = int(plan[0].numel())
     f_traffic, _ = load_traffic(tkey, "spgemm_forward")
     if f_traffic:  # forward: measured (PMC) bytes per launch over its live duration
         extra["fwd_traffic_GB"] = round(f_traffic / 1e9, 3)

@@ -92,6 +92,9 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_VPL8
 #define MAXK_PULL_VPL8 0
 #endif
+#ifndef MAXK_PULL_SEL4  // pull_sel4_kernel: four selectors per thread (aligned selectors)
+#define MAXK_PULL_SEL4 1
+#endif
 #ifndef MAXK_PULL_XCD  // pull_q_kernel: XCD x runs the x-th eighth of the tile sequence
 #define MAXK_PULL_XCD 1
 #endif

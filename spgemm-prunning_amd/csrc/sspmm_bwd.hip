@@ -797,6 +797,76 @@ __global__ __launch_bounds__(kBlock) void pull_sel_kernel(const uint8_t *__restr
     }
 }
 
+// pull_sel_kernel with four selectors per thread (k % 4 == 0, 4-byte aligned selectors): one
+// u32 load and store per thread instead of a byte each, and a destination's 256-bit column
+// set read once per four ranks (ogbn-products-sized, k=32: 2.45M destinations).
+__global__ __launch_bounds__(kBlock) void pull_sel4_kernel(const uint8_t *__restrict__ sel,
+                                                           uint8_t *__restrict__ sel_q,
+                                                           uint8_t *__restrict__ lmap,
+                                                           int64_t num_cols, int k, int kp,
+                                                           int vpl) {
+    __shared__ uint32_t bm[kBlock * 8];  // 256-bit column set per destination (k >= 4)
+    __shared__ uint32_t s_out[kBlock], l_out[kBlock];
+    const int tpd = k / 4;      // threads per destination
+    const int nd = kBlock / tpd;  // destinations per block
+    const int tid = threadIdx.x;
+    const int d = tid / tpd, l0 = (tid % tpd) * 4;
+    const int64_t c0 = (int64_t)blockIdx.x * nd;
+    const int64_t c = c0 + d;
+    const bool act = d < nd && c < num_cols;
+    for (int i = tid; i < nd * 8; i += kBlock) bm[i] = 0u;
+    __syncthreads();
+    const uint32_t w4 = act ? *reinterpret_cast<const uint32_t *>(sel + c * k + l0) : 0u;
+    if (act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t sj = (w4 >> (8 * j)) & 255u;
+            atomicOr(&bm[d * 8 + (sj >> 5)], 1u << (sj & 31));
+        }
+    }
+    __syncthreads();
+    if (act) {
+        uint32_t wds[8];
+        int distinct = 0;
+#pragma unroll
+        for (int wd = 0; wd < 8; ++wd) {
+            wds[wd] = bm[d * 8 + wd];
+            distinct += __popc(wds[wd]);
+        }
+        uint8_t *so = reinterpret_cast<uint8_t *>(s_out), *lo = reinterpret_cast<uint8_t *>(l_out);
+        const int ql = kp / vpl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t sj = (w4 >> (8 * j)) & 255u;
+            const int l = l0 + j;
+            int rank = 0;
+            if (distinct == k) {
+                const int hi = (int)(sj >> 5);
+#pragma unroll
+                for (int wd = 0; wd < 8; ++wd) {
+                    rank += wd < hi ? __popc(wds[wd]) : 0;
+                    rank += wd == hi ? __popc(wds[wd] & ((1u << (sj & 31)) - 1u)) : 0;
+                }
+            } else {  // repeated selectors: rank by (selector, l)
+                for (int m = 0; m < k; ++m) {
+                    const uint32_t sm = sel[c * k + m];
+                    rank += (sm < sj) || (sm == sj && m < l);
+                }
+            }
+            const int h = rank / kp, r = rank % kp;
+            const int slot = h * kp + vpl * (r % ql) + r / ql;
+            so[d * k + slot] = (uint8_t)sj;
+            lo[d * k + slot] = (uint8_t)l;
+        }
+    }
+    __syncthreads();
+    const int64_t nbytes = (num_cols - c0 < nd ? num_cols - c0 : nd) * (int64_t)k;
+    if ((int64_t)tid * 4 < nbytes) {
+        reinterpret_cast<uint32_t *>(sel_q + c0 * k)[tid] = s_out[tid];
+        reinterpret_cast<uint32_t *>(lmap + c0 * k)[tid] = l_out[tid];
+    }
+}
+
 // One tile's entry loop of pull_q_kernel: adds the tile's n_e entries (ers)
 // into the fp64 accumulator, gathering from the slice's G' rows (grs).
 template <int LR, int U, bool FULLD, int VPL>
@@ -1592,9 +1662,16 @@ int pull_impl(const float *grad_out, const float *row_div, const uint8_t *cbsr_i
         const int vpl = kp != 8 ? 4 : MAXK_PULL_VPL8 ? MAXK_PULL_VPL8 : parts == 1 ? 8 : 4;
         lmap = lm;
         if (!front) goto reduce;
-        hipLaunchKernelGGL(pull_sel_kernel, dim3((unsigned)ceil_div(num_cols, nd)), dim3(kBlock),
-                           0, s, cbsr_idx, sel_q, lm, num_cols, k, kp, vpl);
-        MAXK_LAUNCHED("pull_sel_kernel");
+        if (MAXK_PULL_SEL4 && (reinterpret_cast<uintptr_t>(cbsr_idx) & 3) == 0) {
+            const int nd4 = kBlock / (k / 4);
+            hipLaunchKernelGGL(pull_sel4_kernel, dim3((unsigned)ceil_div(num_cols, nd4)),
+                               dim3(kBlock), 0, s, cbsr_idx, sel_q, lm, num_cols, k, kp, vpl);
+            MAXK_LAUNCHED("pull_sel4_kernel");
+        } else {
+            hipLaunchKernelGGL(pull_sel_kernel, dim3((unsigned)ceil_div(num_cols, nd)),
+                               dim3(kBlock), 0, s, cbsr_idx, sel_q, lm, num_cols, k, kp, vpl);
+            MAXK_LAUNCHED("pull_sel_kernel");
+        }
         const int64_t work = tiles * parts;
         const bool fulld = dim_origin == kMaxDim;
         const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(work) : work);

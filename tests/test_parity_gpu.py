@@ -155,6 +155,29 @@ def test_pull_backward_repeats(mk, cuda):
     assert torch.allclose(a, b, rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("dup", [False, True])
+@pytest.mark.parametrize("k", [4, 12, 16, 32, 64, 128])
+def test_pull_selector_kernels(mk, cuda, k, dup):
+    """The pull's selector ordering runs four selectors per thread (pull_sel4_kernel) on a
+    4-byte-aligned selector buffer and one per thread otherwise: both against the oracle, on
+    distinct selectors and on rows with repeated ones (ranked by (selector, l))."""
+    z = load_golden(next(c for c in CASES if "sym_d256_k16" in c))
+    V = z["row_ptr"].size - 1
+    rng = np.random.default_rng(k)
+    sel = np.stack([rng.choice(256, k, replace=False) for _ in range(V)]).astype(np.uint8)
+    if dup:
+        sel[::3, 1] = sel[::3, 0]
+    g = rng.standard_normal((V, 256), dtype=np.float32)
+    args = [T(z[n], cuda) for n in ("row_ptr", "col_idx", "val")]
+    ref = O.sspmm_bwd(z["row_ptr"], z["col_idx"], z["val"], g, sel)
+    aligned = T(sel, cuda)
+    raw = torch.empty(V * k + 1, dtype=torch.uint8, device=cuda)
+    odd = raw[1:].view(V, k)  # contiguous, one byte off the allocation
+    odd.copy_(aligned)
+    for cs in (aligned, odd):
+        close(mk.sspmm_backward(*args, T(g, cuda), cs, mode="pull"), ref)
+
+
 @pytest.mark.parametrize("mode", ["bucket", "pull"])
 @pytest.mark.parametrize("k", [8, 16])
 def test_bucket_backward_many_parts(mk, cuda, k, mode):
