@@ -43,14 +43,14 @@ OP_KERNELS = {
     "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>"],
     # k % 4 == 0: slot-ordered selectors, quantile-slot tiles; else pull_tile_kernel; plus
     # gprime_kernel when a row_div is given (the bench passes none)
-    "sspmm_backward_pull": ["pull_sel_kernel", "pull_q_kernel", "pull_tile_kernel",
-                            "pull_reduce_kernel", "gprime_kernel"],
+    "sspmm_backward_pull": ["pull_q_kernel", "pull_reduce_kernel", "pull_sel4_kernel",
+                            "pull_sel_kernel", "pull_tile_kernel", "gprime_kernel"],
     "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
     # csc over the sparse tiles' edges, then the pull over the dense ones, accumulating
     "sspmm_backward_hybrid": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>",
-                              "pull_sel_kernel", "pull_q_kernel", "pull_reduce_kernel",
-                              "gprime_kernel"],
+                              "pull_sel4_kernel", "pull_sel_kernel", "pull_q_kernel",
+                              "pull_reduce_kernel", "gprime_kernel"],
 }
 
 

@@ -52,3 +52,29 @@ def test_hybrid_against_oracle(cuda, name, density, k, streams, monkeypatch):
     go = O.sspmm_bwd(ip.cpu().numpy(), ix.cpu().numpy(), val.cpu().numpy(), g, ci,
                      row_div=div.cpu().numpy())
     close(gs, go)
+
+
+@pytest.mark.parametrize("k", [16, 32])
+def test_hybrid_rectangular(cuda, k):
+    """A shard's view (maxk_dist): the first rows of the ordered graph against all its
+    columns, so rows != columns and "auto" resolves on the shard's own locality."""
+    import maxk_cuda_kernels as mk
+    ip, ix = _graphs(cuda)["ordered"]
+    V, D = ip.numel() - 1, 256
+    n = V // 3
+    ip_s, ix_s = ip[:n + 1].contiguous(), ix[:int(ip[n])].contiguous()
+    rng = np.random.default_rng(7 + k)
+    val = torch.rand(ix_s.numel(), device=cuda)
+    cv, ci = O.topk(rng.standard_normal((V, D), dtype=np.float32), k)
+    g = rng.standard_normal((n, D), dtype=np.float32)
+    div = torch.clamp(torch.diff(ip_s).float(), min=1.0)
+    for density in (0.3, 1.0, 3.0, 10.0, 30.0):  # the first that pulls some tiles, not all
+        plan = mk.hybrid_plan(ip_s, ix_s, val, V, k, D, density=density, cache=False)
+        if 0 < plan[4].shape[0] < ix_s.numel():
+            break
+    assert 0 < plan[4].shape[0] < ix_s.numel()
+    gs = mk.sspmm_backward(ip_s, ix_s, val, torch.from_numpy(g).to(cuda),
+                           torch.from_numpy(ci).to(cuda), row_div=div, mode="hybrid", plan=plan)
+    go = O.sspmm_bwd(ip_s.cpu().numpy(), ix_s.cpu().numpy(), val.cpu().numpy(), g, ci,
+                     row_div=div.cpu().numpy())
+    close(gs, go)
