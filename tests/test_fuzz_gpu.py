@@ -1,5 +1,5 @@
 """Property-based GPU parity (hypothesis, derandomized so every run draws the same cases): the
-HIP forward, every backward mode and the top-k against the pinned oracle on random graphs
+HIP forward, every backward mode (hybrid included) and the top-k against the pinned oracle on random graphs
 the hand-written cases do not reach -- rectangular (num_cols != num_rows), duplicate edges,
 empty rows, hub rows up to every column, D not a multiple of 4, k from 1 to D, work items
 from 1 token up.  Tolerance as in test_parity_gpu: |hip - oracle| <= 1e-4 * max(1, |oracle|);
@@ -74,4 +74,9 @@ def test_random_graphs_every_mode(cuda, c):
     for mode in modes:
         gs = mk.sspmm_backward(*args, T(g, cuda), T(ci, cuda), row_div=dv, chunk=chunk,
                                mode=mode)
+        close(gs, go)
+    if D % 4 == 0 and k % 4 == 0:  # hybrid: every tile pulled, a mix, or none
+        plan = mk.hybrid_plan(*args, C, k, D, density=(0.0, 0.5, 3.0)[seed % 3], cache=False)
+        gs = mk.sspmm_backward(*args, T(g, cuda), T(ci, cuda), row_div=dv, chunk=chunk,
+                               mode="hybrid", plan=plan)
         close(gs, go)
