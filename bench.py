@@ -167,6 +167,14 @@ def host_info():
             "cores_used": host_cores(), "torch_threads": torch.get_num_threads()}
 
 
+def _order(row_ptr, col):
+    """--reorder's vertex order: maxk_graph.locality_order, or by degree with
+    MAXK_BENCH_ORDER=degree (a probe)."""
+    if os.environ.get("MAXK_BENCH_ORDER") == "degree":
+        return maxk_graph.degree_order(row_ptr)
+    return maxk_graph.locality_order(row_ptr, col)
+
+
 def cpu_spmm_baselines(row_ptr, col, val, dense, target_s=6.0):
     """The reference's CPU SpMM denominators: scipy.sparse CSR @ dense X^ on
     1 thread, and torch.sparse CSR mm on all host threads, each on a leading-row sample of
@@ -297,7 +305,7 @@ def main():
             row_ptr, col = maxk_graph.synthetic_graph(args.graph, args.seed, dev)
             if args.reorder:
                 row_ptr, col, _ = maxk_graph.permute_graph(
-                    row_ptr, col, maxk_graph.locality_order(row_ptr, col))
+                    row_ptr, col, _order(row_ptr, col))
             n_e = torch.tensor([col.numel()], dtype=torch.int64, device=cdev)
         else:
             n_e = torch.zeros(1, dtype=torch.int64, device=cdev)
@@ -319,7 +327,7 @@ def main():
             torch.cuda.synchronize()
             t_r = time.perf_counter()
             row_ptr, col, _ = maxk_graph.permute_graph(
-                row_ptr, col, maxk_graph.locality_order(row_ptr, col))
+                row_ptr, col, _order(row_ptr, col))
             torch.cuda.synchronize()
             t_reorder = time.perf_counter() - t_r
         data += "; vertex order by maxk_graph.locality_order (once per graph, untimed)"

@@ -309,6 +309,13 @@ def locality_order(indptr: torch.Tensor, indices: torch.Tensor, iters: int = 20,
     return torch.argsort(lab * V + torch.arange(V, device=dev))
 
 
+def degree_order(indptr: torch.Tensor) -> torch.Tensor:
+    """Vertices by decreasing degree (ties by id): `perm[new] = old`.  A probe of how much
+    the pull backward gains when heavy destinations share buckets."""
+    deg = torch.diff(indptr.long())
+    return torch.sort(-deg, stable=True).indices
+
+
 def permute_graph(indptr: torch.Tensor, indices: torch.Tensor, perm: torch.Tensor):
     """The CSR of the graph relabelled by `perm` (perm[new] = old): row and column i of the
     result are vertex perm[i].  Returns (indptr int32, indices int32, edge_perm int64) with
