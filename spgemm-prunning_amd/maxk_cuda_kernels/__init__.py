@@ -455,6 +455,39 @@ BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid")
 _LOCALITY: "dict" = {}
 
 
+_SCALED: "dict" = {}
+
+
+def _scaled_entries(ent: torch.Tensor, tiles: torch.Tensor, counts: torch.Tensor, nb: int,
+                    rps: int, row_div: torch.Tensor) -> torch.Tensor:
+    """The pull entries with each weight divided by its source row's row_div, so the tile
+    kernels gather G itself instead of a G / row_div copy (gprime_kernel: a read and a write
+    of all of G per call; ogbn-products 2 x 2.5 GB).  `tiles[i]` is the tile of the entries'
+    i-th run of `counts[i]`.  Cached per entry tensor for one (row_div object, version): the
+    degrees a layer divides by are the same tensor every call (maxk_layers.CSRGraph)."""
+    key = id(ent)
+    hit = _SCALED.get(key)
+    if hit is not None:
+        re, rd, ver, sc = hit
+        if re() is ent and rd() is row_div and ver == row_div._version:
+            return sc
+    t = torch.repeat_interleave(tiles.long(), counts.long())
+    rows = (t // nb) * rps + (ent[:, 0].long() & 0xffff)
+    del t
+    sc = ent.clone()
+    sc[:, 1] = (ent[:, 1].view(torch.float32) / row_div[rows]).view(torch.int32)
+    del rows
+    if key not in _SCALED:
+        weakref.finalize(ent, _SCALED.pop, key, None)
+    _SCALED[key] = (weakref.ref(ent), weakref.ref(row_div), row_div._version, sc)
+    return sc
+
+
+def _prescale() -> bool:
+    """MAXK_PULL_PRESCALE=0 keeps the per-call G / row_div copy instead of scaled entries."""
+    return os.environ.get("MAXK_PULL_PRESCALE", "1") != "0"
+
+
 def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> float:
     """Edges per occupied (source row, bucket of 2^shift columns) pair: how many entries of
     a pull tile share a source row's G lines.  A randomly labelled graph with `a` edges per
@@ -608,9 +641,15 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         ws_bytes = L.maxk_sspmm_backward_pull_tiles_workspace_size(num_rows, num_cols, D, k, n_t)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
 
+        pdiv = row_div
+        if row_div is not None and n_t > 0 and _prescale():
+            ent = _scaled_entries(ent, tl, torch.diff(te), int(L.maxk_bucket_count(num_cols, shift)),
+                                  -(-num_rows // S), row_div)
+            pdiv = None
+
         def tiles(flags):
             _capi.check(L.maxk_sspmm_backward_pull_tiles(
-                _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tl), _ptr(te), n_t,
+                _ptr(grad_output), _ptr(pdiv), _ptr(cbsr_idx), _ptr(tl), _ptr(te), n_t,
                 _ptr(bp), _ptr(bt), _ptr(ent), shift, S, flags, _ptr(out), num_rows, num_cols,
                 ent.shape[0], D, k, _ptr(ws), ws.numel(), _stream(dev)),
                 "maxk_sspmm_backward_pull_tiles")
@@ -637,6 +676,11 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     if mode == "pull":
         tptr, ent, shift, S = (plan if plan is not None else
                                pull_plan(indptr, indices, values, num_cols, k, D))
+        if row_div is not None and E > 0 and _prescale():
+            nb = int(L.maxk_bucket_count(num_cols, shift))
+            ent = _scaled_entries(ent, torch.arange(S * nb, device=dev), torch.diff(tptr), nb,
+                                  -(-num_rows // S), row_div)
+            row_div = None
         ws_bytes = L.maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, D, k, S)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         with torch.cuda.device(dev):

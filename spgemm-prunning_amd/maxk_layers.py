@@ -42,6 +42,13 @@ import maxk_cuda_kernels as mk
 from maxk_spgemm_function import maxk_spgemm
 
 
+def _clamped(graph, name: str) -> torch.Tensor:
+    """graph.<name> clamped to >= 1: CSRGraph's cached tensor, or computed for a graph-like
+    object without the cache."""
+    f = getattr(graph, "clamped", None)
+    return f(name) if f is not None else getattr(graph, name).clamp(min=1.0)
+
+
 class CSRGraph:
     """Adjacency in CSR with rows = destinations: out[r] aggregates x[indices[e]], e in row r."""
 
@@ -57,6 +64,15 @@ class CSRGraph:
         self.out_degrees = torch.bincount(self.indices.long(),
                                           minlength=self.num_nodes).float()
         self._rows = None
+        self._clamped = {}
+
+    def clamped(self, name: str) -> torch.Tensor:
+        """in_degrees / out_degrees clamped to >= 1, built once: the same divisor tensor
+        every call, so per-(plan, divisor) work in the backward (maxk_cuda_kernels'
+        pre-scaled pull entries) is done once per graph."""
+        if name not in self._clamped:
+            self._clamped[name] = getattr(self, name).clamp(min=1.0)
+        return self._clamped[name]
 
     def edge_rows(self) -> torch.Tensor:
         if self._rows is None:
@@ -214,7 +230,7 @@ class MaxKSAGEConv(nn.Module):
         nn.init.xavier_uniform_(self.fc_neigh.weight, gain=gain)
 
     def forward(self, graph: CSRGraph, x_sparse, topk_values, topk_indices):
-        deg = graph.in_degrees.clamp(min=1.0)
+        deg = _clamped(graph, "in_degrees")
         if self.reference_compat:  # :153-181: only h_self sees the dropout
             h_self = self.feat_drop(x_sparse)
         else:
@@ -254,11 +270,11 @@ class MaxKGraphConv(nn.Module):
         if self._graph_key is not graph:  # once per graph, like the reference's set_graph_data
             v = graph.values
             if self._norm in ("left", "both"):
-                src = graph.out_degrees.clamp(min=1.0)
+                src = _clamped(graph, "out_degrees")
                 src = src.pow(-0.5) if self._norm == "both" else 1.0 / src
                 v = v * src[graph.indices.long()]
             if self._norm in ("right", "both"):
-                dst = graph.in_degrees.clamp(min=1.0)
+                dst = _clamped(graph, "in_degrees")
                 dst = dst.pow(-0.5) if self._norm == "both" else 1.0 / dst
                 v = v * dst[graph.edge_rows()]
             self._edge_values, self._graph_key = v.contiguous(), graph
@@ -269,7 +285,7 @@ class MaxKGraphConv(nn.Module):
             # :302-310 normalise feat_src, which the kernel never reads; :341-345 feed it the
             # raw topk_values with the in-degrees as divisor; :381-389 then apply the right
             # normalisation on top
-            deg = graph.in_degrees.clamp(min=1.0)
+            deg = _clamped(graph, "in_degrees")
             rst = graph.aggregate(topk_values, topk_indices, self.in_feats, row_div=deg)
             if self.weight is not None:
                 rst = rst @ self.weight
@@ -303,7 +319,7 @@ class MaxKGINConv(nn.Module):
 
     def forward(self, graph: CSRGraph, x, topk_values, topk_indices):
         # reference_compat: the "sum" kernel call passes the in-degrees (:491-495), a mean
-        row_div = graph.in_degrees.clamp(min=1.0) if self.reference_compat else None
+        row_div = _clamped(graph, "in_degrees") if self.reference_compat else None
         neigh = graph.aggregate(topk_values, topk_indices, x.shape[1], row_div=row_div)
         rst = (1 + self.eps) * x + neigh
         if self.apply_func is not None:

@@ -78,3 +78,34 @@ def test_hybrid_rectangular(cuda, k):
     go = O.sspmm_bwd(ip_s.cpu().numpy(), ix_s.cpu().numpy(), val.cpu().numpy(), g, ci,
                      row_div=div.cpu().numpy())
     close(gs, go)
+
+
+@pytest.mark.parametrize("mode", ["pull", "hybrid"])
+def test_prescaled_entries(cuda, mode, monkeypatch):
+    """With a row_div the pull gathers G itself from entries whose weights are pre-divided
+    (cached per plan and divisor tensor/version) instead of a G / row_div copy: both ways
+    against the oracle, and the cache follows an in-place change of the divisor and a new
+    divisor tensor."""
+    import maxk_cuda_kernels as mk
+    ip, ix = _graphs(cuda)["ordered"]
+    V, D, k = ip.numel() - 1, 256, 16
+    rng = np.random.default_rng(11)
+    val = torch.rand(ix.numel(), device=cuda)
+    cv, ci = O.topk(rng.standard_normal((V, D), dtype=np.float32), k)
+    g = rng.standard_normal((V, D), dtype=np.float32)
+    gt, ct = torch.from_numpy(g).to(cuda), torch.from_numpy(ci).to(cuda)
+    args = (ip.cpu().numpy(), ix.cpu().numpy(), val.cpu().numpy(), g, ci)
+    div = torch.clamp(torch.diff(ip).float(), min=1.0)
+    plan = (mk.hybrid_plan(ip, ix, val, V, k, D, density=0.3) if mode == "hybrid"
+            else mk.pull_plan(ip, ix, val, V, k, D))
+    for pre in ("1", "0"):
+        monkeypatch.setenv("MAXK_PULL_PRESCALE", pre)
+        gs = mk.sspmm_backward(ip, ix, val, gt, ct, row_div=div, mode=mode, plan=plan)
+        close(gs, O.sspmm_bwd(*args, row_div=div.cpu().numpy()))
+    monkeypatch.setenv("MAXK_PULL_PRESCALE", "1")
+    div.mul_(2.0)  # in place: the scaled entries are rebuilt
+    gs = mk.sspmm_backward(ip, ix, val, gt, ct, row_div=div, mode=mode, plan=plan)
+    close(gs, O.sspmm_bwd(*args, row_div=div.cpu().numpy()))
+    div2 = div + 1.0  # another divisor tensor
+    gs = mk.sspmm_backward(ip, ix, val, gt, ct, row_div=div2, mode=mode, plan=plan)
+    close(gs, O.sspmm_bwd(*args, row_div=div2.cpu().numpy()))
