@@ -211,3 +211,37 @@ def test_pull_slice_rule():
     assert L.maxk_sspmm_backward_pull_workspace_size(232965, 232965, 256, 16, 65) == \
         gp + 65 * 228 * (16 << 10) * 4 + selq
     assert L.maxk_sspmm_backward_pull_workspace_size(10, 10, 0, 16, 1) == 0
+
+
+def test_scaled_pull_entries():
+    """The pull entries pre-divided by their source row's row_div (maxk_cuda_kernels.
+    _scaled_entries): entry {row in slice | column << 16, weight bits} of tile t = s*nb + j
+    belongs to row s*rps + (row in slice); the weight becomes weight / row_div[row], the key
+    word is unchanged, and the copy is cached per (entries, divisor tensor, version)."""
+    import maxk_cuda_kernels as mk
+    g = torch.Generator().manual_seed(3)
+    S, nb, rps, V = 3, 4, 5, 13
+    counts = torch.randint(0, 4, (S * nb,), generator=g)
+    E = int(counts.sum())
+    tiles = torch.arange(S * nb)
+    t_of = torch.repeat_interleave(tiles, counts)
+    rin = torch.randint(0, rps, (E,), generator=g)
+    rin = torch.where(t_of // nb * rps + rin < V, rin, 0)
+    col = torch.randint(0, 1 << 10, (E,), generator=g)
+    w = torch.rand(E, generator=g)
+    ent = torch.stack([rin | (col << 16), w.view(torch.int32).long()], 1).to(torch.int32)
+    div = torch.rand(V, generator=g) + 0.5
+    sc = mk._scaled_entries(ent, tiles, counts, nb, rps, div)
+    assert torch.equal(sc[:, 0], ent[:, 0])
+    rows = t_of // nb * rps + rin
+    assert torch.equal(sc[:, 1].view(torch.float32), w / div[rows])
+    assert mk._scaled_entries(ent, tiles, counts, nb, rps, div) is sc  # cached
+    div.mul_(2.0)
+    sc2 = mk._scaled_entries(ent, tiles, counts, nb, rps, div)  # version moved: rebuilt
+    assert torch.equal(sc2[:, 1].view(torch.float32), w / div[rows])
+    # listed tiles (the hybrid): only some tiles, in increasing order
+    lt = torch.tensor([1, 6, 11])
+    sub = torch.cat([ent[int(counts[:t].sum()):int(counts[:t + 1].sum())] for t in lt.tolist()])
+    sc3 = mk._scaled_entries(sub, lt, counts[lt], nb, rps, div)
+    r3 = torch.repeat_interleave(lt, counts[lt]) // nb * rps + (sub[:, 0].long() & 0xffff)
+    assert torch.equal(sc3[:, 1].view(torch.float32), sub[:, 1].view(torch.float32) / div[r3])
