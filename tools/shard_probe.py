@@ -23,12 +23,16 @@ ap.add_argument("--graph", default="reddit")
 ap.add_argument("--k", type=int, default=None)
 ap.add_argument("--worlds", type=int, nargs="*", default=[1, 2, 4, 8])
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--reorder", action="store_true", help="relabel by maxk_graph.locality_order")
 a = ap.parse_args()
 P = maxk_graph.PRESETS[a.graph]
 k = a.k or P["k"]
 D = P["D"]
 dev = torch.device("cuda")
 row_ptr, col = maxk_graph.synthetic_graph(a.graph, device="cuda")
+if a.reorder:
+    row_ptr, col, _ = maxk_graph.permute_graph(row_ptr, col,
+                                               maxk_graph.locality_order(row_ptr, col))
 V, E = row_ptr.numel() - 1, col.numel()
 g = torch.Generator(device=dev).manual_seed(123)
 val = torch.rand(E, generator=g, device=dev)
@@ -52,7 +56,7 @@ def timed(f):
 print(f"{a.graph} V={V} E={E} D={D} k={k}: per-rank compute (fwd + bwd ms), slowest rank")
 base = None
 for world in a.worlds:
-    worst = (0.0, 0.0, 0.0, -1)
+    worst = (0.0, 0.0, 0.0, -1, None)
     for rank in range(world):
         sh = maxk_dist.ShardedMaxK(row_ptr, col, val, rank, world, device=dev, mode="gather")
         cv, ci = mk.topk_cbsr(X, k)  # the gathered CBSR: every vertex's rows, padded layout
@@ -66,16 +70,17 @@ for world in a.worlds:
         y = torch.empty(sh.n_local, D, device=dev)
         gs = torch.empty(sh.n_cols, k, device=dev)
         plan = sh.plan(k, D)
-        mode = mk._bwd_mode(None, k, sh.col_idx.numel(), sh.n_cols, sh.n_local, D)
+        mode = mk._bwd_mode(None, k, sh.col_idx.numel(), sh.n_cols, sh.n_local, D,
+                            (sh.row_ptr, sh.col_idx))
         tf = timed(lambda: mk.spgemm_forward(sh.row_ptr, sh.col_idx, sh.values, cv_all, ci_all, D,
                                              out=y, validate=False))
         tb = timed(lambda: mk.sspmm_backward(sh.row_ptr, sh.col_idx, sh.values, gl, ci_all,
                                              out=gs, validate=False, mode=mode, plan=plan))
         if tf + tb > worst[0] + worst[1]:
-            worst = (tf, tb, sh.col_idx.numel(), rank)
+            worst = (tf, tb, sh.col_idx.numel(), rank, mode)
         del sh, plan, cv_all, ci_all, gl, y, gs
     t = worst[0] + worst[1]
     base = t if world == 1 else base
     eff = f"  compute-only efficiency {base / (world * t):.2f}" if base and world > 1 else ""
     print(f"  N={world}: rank {worst[3]} fwd {worst[0]:.3f} + bwd {worst[1]:.3f} = {t:.3f} ms "
-          f"({worst[2]} edges){eff}", flush=True)
+          f"({worst[2]} edges, bwd {worst[4]}){eff}", flush=True)
