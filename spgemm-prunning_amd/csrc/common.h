@@ -41,6 +41,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_XCD_SUM  // XCD-contiguous work order in the backward's phase 2
 #define MAXK_XCD_SUM 1
 #endif
+#ifndef MAXK_XCD_SUM_RUN  // csc phase 2: blocks per XCD run (0: one contiguous eighth each)
+#define MAXK_XCD_SUM_RUN 64
+#endif
 #ifndef MAXK_BWD_X4  // 4-l-per-lane phase 1 of the two-phase backward (k % 4 == 0)
 #define MAXK_BWD_X4 1
 #endif
@@ -196,6 +199,16 @@ inline int64_t xcd_grid(int64_t blocks) { return (blocks + kXcds - 1) / kXcds * 
 __device__ __forceinline__ int xcd_contiguous_block(int b, int grid) {
     const int per = grid / kXcds;
     return (b % kXcds) * per + b / kXcds;
+}
+// The same inside windows of kXcds * run blocks (grid a multiple of kXcds): each XCD walks
+// runs of `run` consecutive blocks, one run per window, so work whose cost varies along the
+// block sequence (a community-ordered shard: dense destination ranges beside nearly empty
+// ones) still reaches every XCD evenly, which one contiguous eighth per XCD does not.
+__device__ __forceinline__ int xcd_window_block(int b, int grid, int run) {
+    const int w = kXcds * run;
+    const int base = b / w * w;
+    const int ws = grid - base < w ? grid - base : w;
+    return base + xcd_contiguous_block(b - base, ws);
 }
 
 // Raw buffer descriptor over [p, p + bytes), built from wave-uniform values (SGPRs).

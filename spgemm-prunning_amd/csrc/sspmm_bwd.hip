@@ -412,7 +412,9 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
     extern __shared__ int32_t s_eid[];  // STAGED: [kWavesPerBlock][chunk]
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int blk = MAXK_XCD_SUM ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int blk = !MAXK_XCD_SUM      ? (int)blockIdx.x
+                    : MAXK_XCD_SUM_RUN ? xcd_window_block(blockIdx.x, gridDim.x, MAXK_XCD_SUM_RUN)
+                                       : xcd_contiguous_block(blockIdx.x, gridDim.x);
     const int item = blk * kWavesPerBlock + wid;
     if (item >= n_items) return;
     const int64_t total = (int64_t)num_cols + num_e;
