@@ -94,7 +94,7 @@ def _check_graph_once(row_ptr, col_idx, num_cols):
 
 
 def _validate_call(validate, row_ptr, col_idx, num_cols, sel, D):
-    if torch.cuda.is_current_stream_capturing():
+    if ent.is_cuda and torch.cuda.is_current_stream_capturing():
         return  # a range check synchronises the host: impossible inside a hipGraph capture
     if validate if validate is not None else _validate_default():
         _validate_graph(row_ptr, col_idx, num_cols, col_idx.numel())
@@ -464,13 +464,18 @@ def _scaled_entries(ent: torch.Tensor, tiles: torch.Tensor, counts: torch.Tensor
     kernels gather G itself instead of a G / row_div copy (gprime_kernel: a read and a write
     of all of G per call; ogbn-products 2 x 2.5 GB).  `tiles[i]` is the tile of the entries'
     i-th run of `counts[i]`.  Cached per entry tensor for one (row_div object, version): the
-    degrees a layer divides by are the same tensor every call (maxk_layers.CSRGraph)."""
+    degrees a layer divides by are the same tensor every call (maxk_layers.CSRGraph).  None
+    when it would have to be built inside a stream capture."""
     key = id(ent)
     hit = _SCALED.get(key)
     if hit is not None:
         re, rd, ver, sc = hit
         if re() is ent and rd() is row_div and ver == row_div._version:
             return sc
+    if ent.is_cuda and torch.cuda.is_current_stream_capturing():
+        # a hipGraph capture records kernels without running them: a copy built here would
+        # be cached before it holds anything, so the caller keeps the G / row_div route
+        return None
     t = torch.repeat_interleave(tiles.long(), counts.long())
     rows = (t // nb) * rps + (ent[:, 0].long() & 0xffff)
     del t
@@ -643,9 +648,10 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
 
         pdiv = row_div
         if row_div is not None and n_t > 0 and _prescale():
-            ent = _scaled_entries(ent, tl, torch.diff(te), int(L.maxk_bucket_count(num_cols, shift)),
-                                  -(-num_rows // S), row_div)
-            pdiv = None
+            sc = _scaled_entries(ent, tl, torch.diff(te), int(L.maxk_bucket_count(num_cols, shift)),
+                                 -(-num_rows // S), row_div)
+            if sc is not None:
+                ent, pdiv = sc, None
 
         def tiles(flags):
             _capi.check(L.maxk_sspmm_backward_pull_tiles(
@@ -678,9 +684,10 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                                pull_plan(indptr, indices, values, num_cols, k, D))
         if row_div is not None and E > 0 and _prescale():
             nb = int(L.maxk_bucket_count(num_cols, shift))
-            ent = _scaled_entries(ent, torch.arange(S * nb, device=dev), torch.diff(tptr), nb,
-                                  -(-num_rows // S), row_div)
-            row_div = None
+            sc = _scaled_entries(ent, torch.arange(S * nb, device=dev), torch.diff(tptr), nb,
+                                 -(-num_rows // S), row_div)
+            if sc is not None:
+                ent, row_div = sc, None
         ws_bytes = L.maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, D, k, S)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         with torch.cuda.device(dev):

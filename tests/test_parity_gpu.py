@@ -609,6 +609,12 @@ def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch, mode):
     torch.cuda.synchronize()
     close(out, z["y_ref"])
     close(gs, z["grad_cbsr_ref"])
+    # eager after the capture: the pull's pre-divided entries are built now, not in the graph
+    gs2 = mk.sspmm_backward(rp, ci, va, g_in, cs, row_div=deg, plan=plan, mode=mode)
+    close(gs2, z["grad_cbsr_ref"])
+    g.replay()
+    torch.cuda.synchronize()
+    close(gs, z["grad_cbsr_ref"])
 
 
 # --------------------------------------------------------------------------- size-independent
