@@ -94,7 +94,7 @@ def _check_graph_once(row_ptr, col_idx, num_cols):
 
 
 def _validate_call(validate, row_ptr, col_idx, num_cols, sel, D):
-    if ent.is_cuda and torch.cuda.is_current_stream_capturing():
+    if torch.cuda.is_current_stream_capturing():
         return  # a range check synchronises the host: impossible inside a hipGraph capture
     if validate if validate is not None else _validate_default():
         _validate_graph(row_ptr, col_idx, num_cols, col_idx.numel())
