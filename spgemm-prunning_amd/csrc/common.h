@@ -95,6 +95,12 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_VPL8
 #define MAXK_PULL_VPL8 0
 #endif
+#ifndef MAXK_TOPK_BISECT  // four-row top-k: bisection over [lower bound, max] of the keys
+#define MAXK_TOPK_BISECT 1
+#endif
+#ifndef MAXK_TOPK_LB  // four-row top-k: bit search from a lower bound of the k-th key
+#define MAXK_TOPK_LB 1
+#endif
 #ifndef MAXK_PULL_SEL4  // pull_sel4_kernel: four selectors per thread (aligned selectors)
 #define MAXK_PULL_SEL4 1
 #endif

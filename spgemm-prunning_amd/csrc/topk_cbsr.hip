@@ -307,32 +307,69 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         // the row's keys differ: T | bit is kept while at least k keys are >= it (one compare
         // per key and a DPP row sum per bit, no LDS).  A candidate with exactly k keys >= it
         // ends the row's search: selecting key >= T then takes exactly k.
-        uint32_t mx = 0u, mn = ~0u;
+        // The search starts at the highest bit where mx and a lower bound lb of the answer
+        // differ: lb = max(smallest key, smallest over the row's lanes of the lane's j-th
+        // largest key, j = ceil(k / 16)), since 16 lanes x j keys are >= the latter.  The
+        // answer lies in [lb, mx] and so shares their common prefix; on Gaussian rows this
+        // skips the sign and most exponent bits.
+        uint32_t mx = 0u, mn = ~0u, m1 = 0u, m2 = 0u;
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             mx = key[t] > mx ? key[t] : mx;  // columns past D hold key 0
             mn = ok[t] && key[t] < mn ? key[t] : mn;
+            m2 = max(m2, min(m1, key[t]));
+            m1 = max(m1, key[t]);
         }
         mx = row_max(mx);
         mn = row_min(mn);
-        const uint32_t diff = mx ^ mn;
-        int bit = diff ? 31 - __builtin_clz(diff) : -1;
-        // common prefix of the keys (all keys are >= it); bit 31 differing -> no prefix
-        uint32_t thr = !diff ? mx : (bit == 31 ? 0u : mx & (~0u << (bit + 1)));
-        bool done = !live || diff == 0u;
+        uint32_t lb = MAXK_TOPK_LB ? row_min(k <= 16 ? m1 : m2) : 0u;
+        lb = lb > mn ? lb : mn;
+        uint32_t thr;
         int need = k;
-        for (;;) {
-            const bool go = !done && bit >= 0;
-            if (__ballot(go) == 0) break;
-            const uint32_t c = thr | (1u << (bit & 31));
-            uint32_t n = 0;  // columns past D hold key 0 < c (c >= 1): no mask needed
+        if (MAXK_TOPK_BISECT) {
+            // Bisection over the key interval [lb, mx] itself: the answer is the largest c
+            // with at least k keys >= c.  Invariant: >= k keys are >= lo, the answer <= hi.
+            // The bit search below halves a power-of-two interval instead, which is 2^31
+            // wide whenever [lb, mx] straddles a float exponent boundary with a carry (a
+            // Gaussian row's does: 0x3F7F... -> 0x4000...); the count of keys >= mid == k
+            // ends a row early in both.
+            uint32_t lo = lb, hi = mx;
+            bool done = !live || lo == hi;
+            for (;;) {
+                const bool go = !done;
+                if (__ballot(go) == 0) break;
+                const uint32_t d = hi - lo;
+                const uint32_t mid = lo + (d >> 1) + (d & 1u);  // in (lo, hi]: >= 1
+                uint32_t n = 0;  // columns past D hold key 0 < mid: no mask needed
 #pragma unroll
-            for (int t = 0; t < 16; ++t) n += key[t] >= c ? 1u : 0u;
-            n = row_sum(n);
-            if (go) {
-                if (n >= (uint32_t)k) thr = c;
-                if (n == (uint32_t)k) done = true;
-                --bit;
+                for (int t = 0; t < 16; ++t) n += key[t] >= mid ? 1u : 0u;
+                n = row_sum(n);
+                if (go) {
+                    if (n >= (uint32_t)k) lo = mid;
+                    else hi = mid - 1u;
+                    if (n == (uint32_t)k || lo == hi) done = true;
+                }
+            }
+            thr = lo;
+        } else {
+            const uint32_t diff = mx ^ lb;
+            int bit = diff ? 31 - __builtin_clz(diff) : -1;
+            // common prefix of the keys (all keys are >= it); bit 31 differing -> no prefix
+            thr = !diff ? mx : (bit == 31 ? 0u : mx & (~0u << (bit + 1)));
+            bool done = !live || diff == 0u;
+            for (;;) {
+                const bool go = !done && bit >= 0;
+                if (__ballot(go) == 0) break;
+                const uint32_t c = thr | (1u << (bit & 31));
+                uint32_t n = 0;  // columns past D hold key 0 < c (c >= 1): no mask needed
+#pragma unroll
+                for (int t = 0; t < 16; ++t) n += key[t] >= c ? 1u : 0u;
+                n = row_sum(n);
+                if (go) {
+                    if (n >= (uint32_t)k) thr = c;
+                    if (n == (uint32_t)k) done = true;
+                    --bit;
+                }
             }
         }
         const int sh = 0;

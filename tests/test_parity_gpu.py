@@ -501,6 +501,40 @@ def test_topk_ties_nan_and_uint8(mk, cuda):
     assert np.array_equal(vu.cpu().numpy(), np.take_along_axis(xu, order, 1))
 
 
+@pytest.mark.parametrize("D", [256, 100, 64, 7])
+def test_topk_threshold_search_edges(mk, cuda, D):
+    """The threshold search of the top-k kernels (bisection from a lower bound of the k-th
+    key) on rows built to stress it, bit-exact against the oracle for every k up to 32 and a
+    few above: all-equal rows, few distinct values (many ties at the threshold), neighbouring
+    fp32 values (ulp steps), +-inf, -0.0 beside 0.0, NaN, mixed signs, one huge value."""
+    rng = np.random.default_rng(D)
+    rows = [np.full(D, 1.5), np.full(D, -2.0), rng.integers(0, 3, D).astype(np.float64),
+            rng.integers(-2, 2, D) * 0.5,
+            np.nextafter(np.float32(1.0), np.float32(2.0)) + np.arange(D) * 0.0,
+            rng.standard_normal(D), rng.random(D), -rng.random(D)]
+    u = np.float32(1.0)
+    steps = np.array([u] * D, np.float32)
+    for j in range(1, D):  # consecutive floats: keys one apart
+        steps[j] = np.nextafter(steps[j - 1], np.float32(2.0))
+    rows.append(rng.permutation(steps))
+    special = rng.standard_normal(D)
+    special[rng.choice(D, min(D, 6), replace=False)] = [np.inf, -np.inf, np.nan, -0.0, 0.0,
+                                                         3e38][:min(D, 6)]
+    rows.append(special)
+    big = rng.random(D)
+    big[0] = 1e30
+    rows.append(big)
+    x = np.stack(rows).astype(np.float32)
+    x = np.concatenate([x, rng.permutation(x, axis=1)])
+    for k in sorted({1, 2, 3, 4, 7, 8, 15, 16, 17, 31, 32, min(D, 33), min(D, 64), D}):
+        if k > D:
+            continue
+        v, i = mk.topk_cbsr(T(x, cuda), k)
+        cv, ci = O.topk(x, k)
+        assert np.array_equal(i.cpu().numpy(), ci), (D, k)
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), cv.view(np.uint32)), (D, k)
+
+
 def test_scatter_dense_and_selector_gen(mk, cuda):
     rng = np.random.default_rng(4)
     cv, ci = O.topk(rng.standard_normal((100, 256), dtype=np.float32), 16)
