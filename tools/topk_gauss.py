@@ -12,7 +12,7 @@ import maxk_cuda_kernels as mk  # noqa: E402
 g = torch.Generator(device="cuda").manual_seed(0)
 for V in (2_449_029, 232_965):
     x = torch.randn(V, 256, generator=g, device="cuda")
-    for k in (16, 32):
+    for k in (16, 32, 48, 64):
         for _ in range(3):
             mk.topk_cbsr(x, k)
         ts = []
