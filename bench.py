@@ -39,7 +39,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 
 # kernels making up each op of one step (rocprofv3 names, maxk:: namespace)
 OP_KERNELS = {
-    "spgemm_forward": ["cbsr_pack_kernel", "spgemm_fwd_kernel", "slab_fixup_kernel<0>"],
+    "spgemm_forward": ["spgemm_fwd_kernel", "slab_fixup_kernel<0>", "cbsr_pack4_kernel",
+                       "cbsr_pack_kernel"],
     "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>"],
     # k % 4 == 0: slot-ordered selectors, quantile-slot tiles; else pull_tile_kernel; plus
     # gprime_kernel when a row_div is given (the bench passes none)

@@ -95,6 +95,9 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_VPL8
 #define MAXK_PULL_VPL8 0
 #endif
+#ifndef MAXK_PACK4  // forward record pack: four l per thread (k % 4 == 0, aligned CBSR)
+#define MAXK_PACK4 1
+#endif
 #ifndef MAXK_TOPK_BISECT  // four-row top-k: bisection over [lower bound, max] of the keys
 #define MAXK_TOPK_BISECT 1
 #endif

@@ -113,6 +113,73 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack_kernel(const float *__re
     }
 }
 
+// cbsr_pack_kernel with four l per thread (k % 4 == 0, 16-B aligned values, 4-B aligned
+// selectors): one u32 selector load, one float4 value load, one 16-B and one 8-B store per
+// thread.  Duplicates are detected with a 256-bit column set per vertex (atomicOr returns
+// the bit already set); a vertex with any takes the byte loop of cbsr_pack_kernel's rule
+// (the lowest l of a selector carries the sum of its duplicates in l order).
+__global__ __launch_bounds__(kPackBlock) void cbsr_pack4_kernel(const float *__restrict__ cbsr_val,
+                                                            const uint8_t *__restrict__ cbsr_idx,
+                                                            uint8_t *__restrict__ rec,
+                                                            int num_cols, int k, int RS, int D,
+                                                            int trash) {
+    __shared__ uint32_t s_bits[kPackBlock * 8];  // up to kPackBlock vertices (k = 4)
+    __shared__ int s_dup[kPackBlock];
+    const int tpv = k >> 2;          // threads per vertex
+    const int vpw = kPackBlock / tpv;  // vertices per group
+    const int t = threadIdx.x;
+    const int vl = t / tpv, l0 = (t - vl * tpv) * 4;
+    for (int64_t g0 = (int64_t)blockIdx.x * vpw; g0 < num_cols; g0 += (int64_t)gridDim.x * vpw) {
+        const int64_t v = g0 + vl;
+        const bool act = vl < vpw && v < num_cols;
+        for (int i = t; i < vpw * 8; i += kPackBlock) s_bits[i] = 0u;
+        if (t < vpw) s_dup[t] = 0;
+        __syncthreads();
+        uint32_t w = 0u;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (act) {
+            w = *reinterpret_cast<const uint32_t *>(cbsr_idx + v * k + l0);
+            x = *reinterpret_cast<const float4 *>(cbsr_val + v * k + l0);
+            uint32_t dup = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t sj = (w >> (8 * j)) & 255u;
+                const uint32_t old = atomicOr(&s_bits[vl * 8 + (sj >> 5)], 1u << (sj & 31));
+                dup |= (old >> (sj & 31)) & 1u;
+            }
+            if (dup) s_dup[vl] = 1;
+        }
+        __syncthreads();
+        if (act) {
+            float o[4] = {x.x, x.y, x.z, x.w};
+            uint32_t sel[4];
+            const bool any_dup = s_dup[vl] != 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t sj = (w >> (8 * j)) & 255u;
+                bool first = true;
+                if (any_dup) {  // rare
+                    const int l = l0 + j;
+                    const uint8_t *ci = cbsr_idx + v * k;
+                    const float *cv = cbsr_val + v * k;
+                    for (int m = 0; m < l; ++m) first = first && ci[m] != sj;
+                    if (first)
+                        for (int m = l + 1; m < k; ++m)
+                            if (ci[m] == sj) o[j] += cv[m];
+                }
+                const bool keep = first && (int)sj < D;
+                o[j] = keep ? o[j] : 0.f;
+                sel[j] = keep ? sj : (uint32_t)trash;
+            }
+            uint8_t *p = rec + v * RS;
+            *reinterpret_cast<float4 *>(p + 4 * l0) = make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<uint2 *>(p + 4 * k + 2 * l0) =
+                make_uint2(sel[0] | (sel[1] << 16), sel[2] | (sel[3] << 16));
+        }
+        __syncthreads();  // LDS is reused by the next group
+    }
+}
+
 template <int KG, int U, bool WIDE>
 struct EdgeWalker {
     static constexpr int G = kWave / KG;  // edges per wave step
@@ -495,7 +562,16 @@ extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_id
     int32_t *slab_row = reinterpret_cast<int32_t *>(ws + L.row_off);
     hipStream_t s = as_stream(stream);
     const int D = dim_origin, k = dim_k;
-    if (num_cols > 0) {
+    if (num_cols > 0 && MAXK_PACK4 && k % 4 == 0 && ((uintptr_t)cbsr_val & 15) == 0 &&
+        ((uintptr_t)cbsr_idx & 3) == 0) {
+        const int vpw = kPackBlock / (k / 4);
+        const int64_t groups = ceil_div(num_cols, (int64_t)vpw);
+        hipLaunchKernelGGL(cbsr_pack4_kernel,
+                           dim3((unsigned)(groups < MAXK_PACK_GRID ? groups : MAXK_PACK_GRID)),
+                           dim3(kPackBlock), 0,
+                           s, cbsr_val, cbsr_idx, rec, (int)num_cols, k, L.RS, D, L.DS - 1);
+        MAXK_LAUNCHED("cbsr_pack4_kernel");
+    } else if (num_cols > 0) {
         const int vpw = k >= kPackBlock / kPackMaxV ? kPackBlock / k : kPackMaxV;
         const int64_t groups = ceil_div(num_cols, (int64_t)vpw);
         hipLaunchKernelGGL(cbsr_pack_kernel,

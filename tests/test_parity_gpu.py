@@ -442,6 +442,29 @@ def test_duplicate_selectors_accumulate(mk, cuda):
     close(gs, go)
 
 
+@pytest.mark.parametrize("k", [4, 12, 16, 32])
+def test_forward_pack_aligned_and_not(mk, cuda, k):
+    """The forward's record pack runs four l per thread (cbsr_pack4_kernel) on aligned CBSR
+    buffers and one per thread otherwise: both against the oracle, with repeated selectors
+    on some rows and selectors past D."""
+    rng = np.random.default_rng(31 + k)
+    V, D = 300, 100
+    row_ptr, col = rand_graph(rng, V, 25)
+    val = rng.random(col.size, dtype=np.float32)
+    cv = rng.standard_normal((V, k)).astype(np.float32)
+    ci = np.stack([rng.choice(256, k, replace=False) for _ in range(V)]).astype(np.uint8)
+    ci[::5, 1] = ci[::5, 0]  # duplicates
+    ci[::7, 2] = 200         # past D
+    ref = O.spgemm_fwd(row_ptr, col, val, cv, ci, 256)[:, :D]  # selectors >= D drop out
+    args = (T(row_ptr, cuda), T(col, cuda), T(val, cuda))
+    close(mk.spgemm_forward(*args, T(cv, cuda), T(ci, cuda), D, validate=False), ref)
+    fv = torch.empty(V * k + 1, device=cuda)[1:].view(V, k)  # 4-B, not 16-B aligned
+    fi = torch.empty(V * k + 1, dtype=torch.uint8, device=cuda)[1:].view(V, k)
+    fv.copy_(T(cv, cuda))
+    fi.copy_(T(ci, cuda))
+    close(mk.spgemm_forward(*args, fv, fi, D, validate=False), ref)
+
+
 def test_selectors_past_D_read_zero(mk, cuda):
     """A selector >= D (possible when D < 256; the reference does no bounds check,
     cuda_kernel_bindings.cpp:106-161) contributes nothing, in the forward and in every
