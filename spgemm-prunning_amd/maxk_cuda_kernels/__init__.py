@@ -600,9 +600,10 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                    mode: Optional[str] = None, plan=None) -> torch.Tensor:
     """grad_cbsr[num_cols, k] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]].
 
-    mode "auto" (default; MAXK_BWD_MODE overrides): "pull" or "csc", see _bwd_mode.
+    mode "auto" (default; MAXK_BWD_MODE overrides): "pull", "hybrid" or "csc", see _bwd_mode.
     mode "pull": per tile (row slice, destination bucket), the k values of every edge
-    gathered from G / row_div and summed in fp64 LDS accumulators, no contribution rows;
+    gathered from G and summed in fp64 LDS accumulators, no contribution rows (with a
+    row_div the plan's weights are pre-divided, once per divisor: _scaled_entries);
     uses the graph's pull plan (built once per (indptr, indices, values) and cached, or
     `plan=` from pull_plan()); fp64 tile sums, so two runs agree except in rare rounding
     ties (use "csc" for bitwise repeatability).
@@ -611,9 +612,9 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     mode "csc": two-phase, atomic-free and bitwise deterministic, using the graph's
     transpose plan (built once and cached, or `plan=` from transpose_plan()).
     mode "atomic": one global fp32 atomic per (edge, l); no preprocessing.
-    mode "hybrid" (k % 4 == 0; "auto" picks it on sparse graphs with locality): the pull over the dense
-    tiles of the pull plan and csc over the other edges (hybrid_plan), for large graphs whose
-    vertex order groups their communities."""
+    mode "hybrid" (k % 4 == 0; "auto" picks it on sparse graphs with locality): the pull
+    over the dense tiles of the pull plan, on a second stream, beside csc over the other
+    edges (hybrid_plan), for large graphs whose vertex order groups their communities."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32), (grad_output, "grad_output", torch.float32),
                      (cbsr_idx, "sparse_selector", torch.uint8)):
