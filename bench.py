@@ -82,9 +82,68 @@ def alg_bytes(V, E, D, k, Vc=None):
     return fwd, bwd
 
 
+def compulsory_bytes(V, E, D, k, Vc=None):
+    """Bytes each op must move at least once (no re-reads): row_ptr, col_idx + val, the CBSR
+    once (k f32 + k u8 per vertex; the backward reads only the selectors), the dense [V, D]
+    output (forward) or input G (backward) once, and the [Vc, k] gradient write."""
+    Vc = V if Vc is None else Vc
+    fwd = 4 * (V + 1) + 8 * E + 5 * k * Vc + 4 * V * D
+    bwd = 4 * (V + 1) + 8 * E + k * Vc + 4 * V * D + 4 * Vc * k
+    return fwd, bwd
+
+
 # --------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
-    """Oracle (port of the reference kernels' semantics, 1 thread) on a row sample sized
+def reference_cpu_path(row_ptr, col, val, cv, ci, G, D, deg, target_s=12.0):
+    """The reference's own CPU path for one MaxK aggregation, forward + backward, restated in
+    torch (maxk_spgemm_function.py:96-125 with MAXK_KERNELS_AVAILABLE False, the path its CPU
+    runs take): the top-k scattered into a dense [V, D] input, a coalesced COO adjacency,
+    torch.sparse.mm, / in_degrees; the backward is autograd through that forward (the
+    reference's hand-written backward raises), i.e. A^T (G / deg) gathered at
+    the selectors.  On every host core this process is allotted, on a leading-row sample of
+    the same graph sized for ~target_s seconds; the COO build (a Python loop over rows in the
+    reference) is outside the timing."""
+    rp = row_ptr.cpu().long()
+    c, v = col.cpu().long(), val.cpu()
+    V = rp.numel() - 1
+    E = int(rp[-1])
+    cvn, cin, Gn, dg = cv.cpu(), ci.cpu().long(), G.cpu(), deg.cpu().float().clamp(min=1)
+    nt = host_cores()
+    old_nt = torch.get_num_threads()
+    torch.set_num_threads(nt)
+
+    def run(r1):
+        e1 = int(rp[r1])
+        rows = torch.repeat_interleave(torch.arange(r1), torch.diff(rp[:r1 + 1]))
+        A = torch.sparse_coo_tensor(torch.stack([rows, c[:e1]]), v[:e1], (r1, V)).coalesce()
+        tv = cvn.clone().requires_grad_(True)
+        t0 = time.perf_counter()
+        xs = torch.zeros(V, D).scatter(1, cin, tv)
+        out = torch.sparse.mm(A, xs) / dg[:r1].unsqueeze(-1)
+        t1 = time.perf_counter()
+        out.backward(Gn[:r1])
+        t2 = time.perf_counter()
+        return t1 - t0, t2 - t1, e1
+
+    try:
+        r_cal = max(1, int(np.searchsorted(rp.numpy(), E // 400)))
+        tf, tb, e_cal = run(r_cal)
+        per_edge = (tf + tb) / max(1, e_cal)
+        r1 = int(np.searchsorted(rp.numpy(), min(E, int(target_s / per_edge))))
+        r1 = max(1, min(r1, V))
+        tf, tb, es = run(r1)
+    finally:
+        torch.set_num_threads(old_nt)
+    return {"value": round(2 * es / (tf + tb) / 1e9, 6), "unit": "GTEPS", "cores": nt,
+            "kind": "port",
+            "sample": (f"reference CPU path (maxk_spgemm_function.py:96-125 + autograd backward: "
+                       f"scatter, coalesced-COO torch.sparse.mm, /deg), {nt} threads, rows "
+                       f"[0,{r1}) of the same graph = {es} of {E} edges ({100.0 * es / E:.1f}%); "
+                       f"fwd {tf:.2f}s, bwd {tb:.2f}s")}
+
+
+def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0, deg=None):
+    """The reference's CPU path (reference_cpu_path, the headline value), and beside it the
+    oracle (the port of the reference kernels' semantics, 1 thread) on a row sample sized
     for ~target_s seconds of CPU work; returns the cpu_baseline JSON object."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -111,7 +170,9 @@ def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
     r1 = max(1, min(r1, len(rp) - 1))
     tf, tb = run(r1)
     es = int(rp[r1])
-    out = {
+    out = reference_cpu_path(row_ptr, col, val, cv, ci, G, D,
+                             torch.diff(row_ptr) if deg is None else deg, target_s)
+    out["oracle"] = {
         "value": round(2 * es / (tf + tb) / 1e9, 6), "unit": "GTEPS", "cores": 1, "kind": "port",
         "sample": (f"oracle/maxk_oracle.c fwd SpGEMM + bwd SSpMM (push), 1 thread, rows [0,{r1}) "
                    f"of the same graph = {es} of {E} edges ({100.0 * es / E:.1f}%); "
@@ -134,7 +195,7 @@ def cpu_baseline(row_ptr, col, val, cv, ci, G, D, target_s=12.0):
     O.sspmm_bwd_pull(t_ptr, t_src, t_val, Gn, cin)
     t2 = time.perf_counter()
     O.set_num_threads(1)
-    out["multi_thread"] = {"value": round(2 * E / (t2 - t0) / 1e9, 6), "cores": nt,
+    out["oracle"]["multi_thread"] = {"value": round(2 * E / (t2 - t0) / 1e9, 6), "cores": nt,
                            "sample": f"whole graph, {nt} OpenMP threads (backward in pull form); "
                                      f"fwd {t1 - t0:.2f}s, bwd {t2 - t1:.2f}s"}
     out["host"] = host_info()
@@ -283,6 +344,12 @@ def main():
             dist.init_process_group(backend)
 
     import maxk_cuda_kernels as mk
+    build_cfg = mk._lib().maxk_build_config().decode()
+    if build_cfg and "MAXK_HIP_LIB" not in os.environ:
+        # the product library carries no tuning / ablation macros (tools/tune.sh variants are
+        # selected with MAXK_HIP_LIB and say so in extra.build_config)
+        raise SystemExit(f"libmaxk_hip.so was built with EXTRA_HIPFLAGS={build_cfg!r}; "
+                         "rebuild it with `make -C spgemm-prunning_amd` before benchmarking")
 
     P = dict(maxk_graph.PRESETS[args.graph])
     D = args.dim or P["D"]
@@ -291,19 +358,25 @@ def main():
     t0 = time.time()
     gdir = maxk_graph.find_graph(args.graph, [args.graph_dir] if args.graph_dir else [])
     if gdir:
-        g = maxk_graph.GraphDataLoader(gdir).load_graph(args.graph)
-        row_ptr = torch.from_numpy(g["indptr"]).to(dev)
-        col = torch.from_numpy(g["indices"]).to(dev)
-        V = g["v_num"]
-        data = f"real graph {gdir}/{args.graph}.indptr|.indices; synthetic features"
-    elif world == 1:
-        row_ptr, col = maxk_graph.synthetic_graph(args.graph, args.seed, dev)
-        data = "synthetic"
+        V = maxk_graph.read_binary_array(
+            os.path.join(gdir, f"{os.path.basename(args.graph)}.indptr")).size - 1
+
+    def load_graph():
+        if gdir:
+            g = maxk_graph.GraphDataLoader(gdir).load_graph(args.graph)
+            return (torch.from_numpy(g["indptr"]).to(dev), torch.from_numpy(g["indices"]).to(dev),
+                    f"real graph {gdir}/{args.graph}.indptr|.indices; synthetic features")
+        rp_, col_ = maxk_graph.synthetic_graph(args.graph, args.seed, dev)
+        return rp_, col_, "synthetic"
+
+    if world == 1:
+        row_ptr, col, data = load_graph()
     else:
-        # one rank builds the graph, the others receive it (one broadcast of row_ptr + col)
+        # one rank loads (or builds) the graph and relabels it if asked, the others receive it
+        # (one broadcast of row_ptr + col): every rank shards the same vertex order
         cdev = dev if backend == "nccl" else torch.device("cpu")
         if rank == 0:
-            row_ptr, col = maxk_graph.synthetic_graph(args.graph, args.seed, dev)
+            row_ptr, col, data = load_graph()
             if args.reorder:
                 row_ptr, col, _ = maxk_graph.permute_graph(
                     row_ptr, col, _order(row_ptr, col))
@@ -321,7 +394,8 @@ def main():
                 h = t.cpu()
                 dist.broadcast(h, 0)
                 t.copy_(h)
-        data = "synthetic (built on rank 0, broadcast)"
+        data = (f"real graph {gdir}/{args.graph}.indptr|.indices; synthetic features"
+                if gdir else "synthetic") + " (loaded on rank 0, broadcast)"
     t_reorder = None
     if args.reorder:
         if world == 1:
@@ -459,9 +533,10 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     value = 2.0 * E * args.steps / elapsed / 1e9
     B_f, B_b = alg_bytes(nl, El, D, k, n_cols)
+    C_f, C_b = compulsory_bytes(nl, El, D, k, n_cols)
     bwd_op = f"sspmm_backward_{args.bwd_mode}"
-    op, t_dom, B_dom = (bwd_op, bwd_avg, B_b) if bwd_avg >= fwd_avg else \
-        ("spgemm_forward", fwd_avg, B_f)
+    op, t_dom, B_dom, C_dom = (bwd_op, bwd_avg, B_b, C_b) if bwd_avg >= fwd_avg else \
+        ("spgemm_forward", fwd_avg, B_f, C_f)
     achieved = B_dom / (t_dom * 1e-3) / 1e9
     tkey = f"{args.graph}-D{D}-k{k}-{args.bwd_mode}-n{world}"
     traffic, traffic_src = load_traffic(tkey, op)
@@ -474,6 +549,8 @@ def main():
         "fwd_alg_GBs": round(B_f / fwd_avg / 1e6, 1), "bwd_alg_GBs": round(B_b / bwd_avg / 1e6, 1),
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
         "bwd_mode": args.bwd_mode, "backward_plan_s": round(t_plan, 4),
+        "build_config": build_cfg, "fwd_compulsory_GBs": round(C_f / fwd_avg / 1e6, 1),
+        "bwd_compulsory_GBs": round(C_b / bwd_avg / 1e6, 1),
     }
     if args.reorder:
         extra["reorder_s"] = None if t_reorder is None else round(t_reorder, 3)
@@ -485,8 +562,8 @@ def main():
         extra["hybrid_pull_tiles"] = int(plan[0].numel())
     f_traffic, _ = load_traffic(tkey, "spgemm_forward")
     if f_traffic:  # forward: measured (PMC) bytes per launch over its live duration
-        extra["fwd_traffic_GB"] = round(f_traffic / 1e9, 3)
-        extra["fwd_traffic_GBs"] = round(f_traffic / (fwd_avg * 1e-3) / 1e9, 1)
+        extra["fwd_l2_miss_GB"] = round(f_traffic / 1e9, 3)
+        extra["fwd_l2_miss_GBs"] = round(f_traffic / (fwd_avg * 1e-3) / 1e9, 1)
     if world > 1:
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
                       "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
@@ -514,26 +591,31 @@ def main():
             t_algs, y_lib = mkt.library_spmm_times(row_ptr, col, val, dense, 5, 10)
             rs = t_algs["default"]
             best_alg, rs_best = mkt.best_library(t_algs)
-            err = ((y_lib - y).abs() / y.abs().clamp(min=1)).max().item()
-            extra.update({"rocsparse_spmm_ms": round(rs, 4),
-                          "rocsparse_spmm_ms_best": round(rs_best, 4),
+            err = (None if y_lib is None else
+                   ((y_lib - y).abs() / y.abs().clamp(min=1)).max().item())
+
+            def rnd(a, b=1.0, n=3):  # None when the library refused the algorithm(s)
+                return None if a is None else round(a / b, n)
+            extra.update({"rocsparse_spmm_ms": rnd(rs, n=4),
+                          "rocsparse_spmm_ms_best": rnd(rs_best, n=4),
                           "rocsparse_best_alg": best_alg,
-                          "rocsparse_spmm_ms_by_alg": {a: (None if t is None else round(t, 4))
-                                                       for a, t in t_algs.items()},
-                          "speedup_fwd_vs_rocsparse": round(rs / fwd_avg, 3),
-                          "speedup_bwd_vs_rocsparse": round(rs / bwd_avg, 3),
+                          "rocsparse_spmm_ms_by_alg": {a: rnd(t, n=4) for a, t in t_algs.items()},
+                          "speedup_fwd_vs_rocsparse": rnd(rs, fwd_avg),
+                          "speedup_bwd_vs_rocsparse": rnd(rs, bwd_avg),
                           # the step against two library SpMMs (A X and A^T G; the symmetric
                           # synthetic graph gives A^T the same sparsity)
-                          "speedup_step_vs_rocsparse": round(2 * rs / (fwd_avg + bwd_avg), 3),
-                          "speedup_fwd_vs_rocsparse_best": round(rs_best / fwd_avg, 3),
-                          "speedup_bwd_vs_rocsparse_best": round(rs_best / bwd_avg, 3),
-                          "speedup_step_vs_rocsparse_best": round(2 * rs_best / (fwd_avg + bwd_avg), 3),
+                          "speedup_step_vs_rocsparse": rnd(None if rs is None else 2 * rs,
+                                                           fwd_avg + bwd_avg),
+                          "speedup_fwd_vs_rocsparse_best": rnd(rs_best, fwd_avg),
+                          "speedup_bwd_vs_rocsparse_best": rnd(rs_best, bwd_avg),
+                          "speedup_step_vs_rocsparse_best": rnd(
+                              None if rs_best is None else 2 * rs_best, fwd_avg + bwd_avg),
                           "rocsparse_vs_maxk_max_rel_err": err})
             del dense, y_lib
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(row_ptr, col, val, cv_all, ci_all, G, D, args.cpu_seconds)
+        cpu = cpu_baseline(row_ptr, col, val, cv_all, ci_all, G, D, args.cpu_seconds, deg=deg)
         if not args.no_cpu_spmm:
             extra.update(cpu_spmm_baselines(row_ptr, col, val, mk.cbsr_scatter_dense(cv_all, ci_all, D)))
 
@@ -554,12 +636,18 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "op": op, "kernels": OP_KERNELS[op],
                          "alg_bytes_per_launch": B_dom, "launch_ms": round(t_dom, 4),
+                         # the bytes the op must move once (no re-reads) over its duration
+                         "compulsory_bytes_per_launch": C_dom,
+                         "compulsory_GBs": round(C_dom / (t_dom * 1e-3) / 1e9, 1),
                          "traffic_source": traffic_src, "traffic_key": tkey,
-                         # measured (PMC) bytes per launch over the same live duration
-                         "traffic_GBs": (round(traffic / (t_dom * 1e-3) / 1e9, 1)
+                         # `traffic` is L2 -> fabric bytes (PMC FETCH_SIZE x2 + WRITE_SIZE): it
+                         # counts Infinity-Cache hits too (MI355X_MICROARCH.md, HBM), so it is
+                         # an L2-miss rate, not HBM traffic
+                         "l2_miss_GBs": (round(traffic / (t_dom * 1e-3) / 1e9, 1)
                                          if traffic else None),
-                         "traffic_frac": (round(traffic / (t_dom * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                          if traffic else None)},
+                         "l2_miss_frac_of_hbm_peak": (
+                             round(traffic / (t_dom * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if traffic else None)},
             "cpu_baseline": cpu,
             "extra": extra,
         }

@@ -49,6 +49,10 @@ int maxk_device_count(void);
  * C-locale path order), so a test can tell a stale binary from one built from the tree. */
 const char *maxk_source_digest(void);
 
+/* The extra compiler flags (EXTRA_HIPFLAGS: MAXK_* tuning / ablation macros) this library was
+ * built with; "" for the product build.  The digest above covers them too. */
+const char *maxk_build_config(void);
+
 /* ---------------------------------------------------------------------------
  * Forward row-wise-product SpGEMM:  out = diag(1/row_div) . A . scatter(cbsr)
  *   out[r, cbsr_idx[c,l]] += edge_val[e] * cbsr_val[c,l]   (e in row r, c = col_idx[e])

@@ -27,6 +27,13 @@ extern "C" int maxk_version(void) { return 100; }
 #endif
 extern "C" const char *maxk_source_digest(void) { return MAXK_SRC_DIGEST; }
 
+// EXTRA_HIPFLAGS the library was built with ("" for the product build): every MAXK_* tuning
+// or ablation macro set away from its default in common.h shows here.
+#ifndef MAXK_BUILD_FLAGS
+#define MAXK_BUILD_FLAGS "unknown"
+#endif
+extern "C" const char *maxk_build_config(void) { return MAXK_BUILD_FLAGS; }
+
 extern "C" const char *maxk_last_error(void) { return maxk::g_err; }
 
 extern "C" int maxk_device_count(void) {

@@ -148,7 +148,16 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #define MAXK_BUCKET_PARTS 4
 #endif
 #ifndef MAXK_TOPK_ROWS4  // top-k: 4 rows per wave on 16-lane DPP rows (0: one row per wave)
-#define MAXK_TOPK_ROWS4 1  // (used for k <= 32)
+#define MAXK_TOPK_ROWS4 1
+#endif
+#ifndef MAXK_TOPK_ROWS4_KMAX  // ... for k up to this (at most 64; k=64 ties one row per wave)
+#define MAXK_TOPK_ROWS4_KMAX 48
+#endif
+#ifndef MAXK_TOPK_DIAG  // tools only: four-row top-k search state in idx32 instead of indices
+#define MAXK_TOPK_DIAG 0
+#endif
+#ifndef MAXK_TOPK_FENCE_WAIT  // tools only: s_waitcnt lgkmcnt(0) in the four-row top-k's fences
+#define MAXK_TOPK_FENCE_WAIT 0
 #endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0

@@ -1574,12 +1574,12 @@ int pull_parts(int k, int shift) {
 
 namespace maxk {
 namespace {
-// Workspace of the pull for `tiles` tile partials: G' (row_div), the partials, slot-ordered
-// selectors and their l map.
+// Workspace of the pull for `tiles` tile partials of 2^shift destinations each: G' (row_div),
+// the partials, slot-ordered selectors and their l map.  The size functions pass the largest
+// shift any plan may carry (tiles x 2^shift never shrinks as the shift grows: the columns are
+// rounded up to whole buckets), a call its own plan's shift.
 size_t pull_workspace(int64_t num_rows, int64_t num_cols, int32_t dim_origin, int32_t dim_k,
-                      int64_t tiles) {
-    // the largest shift any plan may carry bounds the tile partials
-    const int shift = std::max(maxk_bucket_shift(dim_k), maxk_pull_shift(dim_k));
+                      int64_t tiles, int shift) {
     const size_t gp = ((size_t)num_rows * dim_origin * sizeof(float) + 255) & ~(size_t)255;
     const size_t tb = (size_t)tiles * ((size_t)dim_k << shift) * sizeof(float);
     // slot-ordered selectors and their l map (pull_sel_kernel), k % 4 == 0
@@ -1622,7 +1622,7 @@ int pull_impl(const float *grad_out, const float *row_div, const uint8_t *cbsr_i
                              (n_list == 0 || (tile_list && bucket_tiles))),
                  "listed tiles need dim_k %% 4 == 0 and tile_list/bucket_ptr/bucket_tiles");
     const int64_t tiles = listed ? (int64_t)n_list : (int64_t)slices * nb;
-    const size_t need = pull_workspace(num_rows, num_cols, dim_origin, dim_k, tiles);
+    const size_t need = pull_workspace(num_rows, num_cols, dim_origin, dim_k, tiles, bucket_shift);
     MAXK_REQUIRE(workspace && workspace_bytes >= need,
                  "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
     // accumulate: bit 0 adds onto grad_cbsr; bit 1 (MAXK_PULL_NO_REDUCE) stops at the tile
@@ -1744,7 +1744,7 @@ extern "C" size_t maxk_sspmm_backward_pull_workspace_size(int64_t num_rows, int6
     if (num_rows < 0 || num_cols < 0 || dim_origin <= 0 || dim_k <= 0 || slices <= 0) return 0;
     const int shift = std::max(maxk_bucket_shift(dim_k), maxk_pull_shift(dim_k));
     return pull_workspace(num_rows, num_cols, dim_origin, dim_k,
-                          (int64_t)slices * maxk_bucket_count(num_cols, shift));
+                          (int64_t)slices * maxk_bucket_count(num_cols, shift), shift);
 }
 
 extern "C" int maxk_sspmm_backward_pull(const float *grad_out, const float *row_div,
@@ -1765,7 +1765,8 @@ extern "C" size_t maxk_sspmm_backward_pull_tiles_workspace_size(int64_t num_rows
                                                                 int32_t dim_origin,
                                                                 int32_t dim_k, int32_t n_tiles) {
     if (num_rows < 0 || num_cols < 0 || dim_origin <= 0 || dim_k <= 0 || n_tiles < 0) return 0;
-    return pull_workspace(num_rows, num_cols, dim_origin, dim_k, n_tiles);
+    return pull_workspace(num_rows, num_cols, dim_origin, dim_k, n_tiles,
+                          std::max(maxk_bucket_shift(dim_k), maxk_pull_shift(dim_k)));
 }
 
 extern "C" int maxk_sspmm_backward_pull_tiles(

@@ -5,8 +5,8 @@
 // kernel topk (kernels/maxk_kernel.cu:23-96), which is approximate (quantised
 // input, index-order output, unfilled slots on ties) -- this one is exact.
 //
-// Two kernels.  topk_rows4_kernel (k <= 32) puts four rows on one wave, 16 lanes per row,
-// and finds the threshold by a bitwise search over DPP row sums (see its comment).
+// Two kernels.  topk_rows4_kernel (k <= MAXK_TOPK_ROWS4_KMAX, 48) puts four rows on one wave,
+// 16 lanes per row, and finds the threshold by bisection over DPP row sums (see its comment).
 // topk_cbsr_kernel (k > 32): one wavefront per row (D <= 256, so <= 4 elements per lane,
 // column j = lane + 64*i for coalesced loads):
 //  1. order-preserving 32-bit keys (NaN above +inf, as torch ranks it);
@@ -264,7 +264,14 @@ __device__ __forceinline__ void load_row16(const T *__restrict__ xr, int D, int 
     }
 }
 
-template <typename T, bool VEC>
+#if MAXK_TOPK_FENCE_WAIT  // tools only: drain the wave's LDS queue at every fence
+#define wave_lds_fence()                                  \
+    do {                                                  \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+        maxk::wave_lds_fence();                           \
+    } while (0)
+#endif
+template <typename T, bool VEC, int J>
 __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict__ x, int64_t ld_x,
                                                             T *__restrict__ out_val,
                                                             uint8_t *__restrict__ out_idx,
@@ -312,17 +319,27 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         // largest key, j = ceil(k / 16)), since 16 lanes x j keys are >= the latter.  The
         // answer lies in [lb, mx] and so shares their common prefix; on Gaussian rows this
         // skips the sign and most exponent bits.
-        uint32_t mx = 0u, mn = ~0u, m1 = 0u, m2 = 0u;
+        // m[0..J) = the lane's J largest keys (an insertion network, lowest slot first so
+        // every slot reads the previous key's values); the lane's j-th largest with
+        // j = ceil(k / 16) <= J bounds the answer from below: 16 lanes x j keys are >= the
+        // smallest of them over the row, and 16 j >= k.
+        uint32_t mx = 0u, mn = ~0u, m[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) m[j] = 0u;
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
             mx = key[t] > mx ? key[t] : mx;  // columns past D hold key 0
             mn = ok[t] && key[t] < mn ? key[t] : mn;
-            m2 = max(m2, min(m1, key[t]));
-            m1 = max(m1, key[t]);
+#pragma unroll
+            for (int j = J - 1; j > 0; --j) m[j] = max(m[j], min(m[j - 1], key[t]));
+            m[0] = max(m[0], key[t]);
         }
         mx = row_max(mx);
         mn = row_min(mn);
-        uint32_t lb = MAXK_TOPK_LB ? row_min(k <= 16 ? m1 : m2) : 0u;
+        uint32_t mj = m[0];
+#pragma unroll
+        for (int j = 1; j < J; ++j) mj = k > 16 * j ? m[j] : mj;
+        uint32_t lb = MAXK_TOPK_LB ? row_min(mj) : 0u;
         lb = lb > mn ? lb : mn;
         uint32_t thr;
         int need = k;
@@ -387,10 +404,15 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         for (int t = 0; t < 16; ++t) neq += (ok[t] && (key[t] >> sh) == T_) ? 1u : 0u;
         const uint32_t neq_row = row_sum(neq);  // every lane: DPP reads the whole row
         const bool ties = live && neq_row != (uint32_t)need;
+        // A row past the end (the last row group's dead sub-rows) takes nothing: its search
+        // never ran (thr = its lower bound), so "key >= thr" would take 32-100 winners and
+        // its compaction would run past its 3*k4 LDS words into the next wave's winners --
+        // which that wave, one grid-stride round behind, may still be ranking (r02's k = 48
+        // mismatch: row 2186888 of the seed-0 [2449029, 256] Gaussian input).
         bool take[16];
         if (__ballot(ties) == 0) {
 #pragma unroll
-            for (int t = 0; t < 16; ++t) take[t] = ok[t] && (key[t] >> sh) >= T_;
+            for (int t = 0; t < 16; ++t) take[t] = live && ok[t] && (key[t] >> sh) >= T_;
         } else {  // rank the equal keys in column order: chunk i, then lane, then j
             uint32_t base = 0;
 #pragma unroll
@@ -403,7 +425,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
                 for (int j = 0; j < 4; ++j) {
                     const int t = 4 * i + j;
                     const bool eq = ok[t] && (key[t] >> sh) == T_;
-                    take[t] = (ok[t] && (key[t] >> sh) > T_) || (eq && r < (uint32_t)need);
+                    take[t] = live && ((ok[t] && (key[t] >> sh) > T_) || (eq && r < (uint32_t)need));
                     r += eq ? 1u : 0u;
                 }
                 base += row_sum(c);
@@ -434,6 +456,21 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
 #pragma unroll
         for (int t = 0; t < 16; ++t) nw += take[t] ? 1u : 0u;
         uint32_t slot = row_prefix_excl(nw);
+#if MAXK_TOPK_DIAG == 1  // tools only: per-row search state in idx32 (its top-k copy not written)
+        {
+            const uint32_t tot = row_sum(nw);
+            if (out_idx32 && live && q == 0) {
+                int32_t *d = out_idx32 + (int64_t)row * k;
+                d[0] = (int32_t)tot;
+                d[1] = (int32_t)thr;
+                d[2] = need;
+                d[3] = ties ? 1 : 0;
+                d[4] = (int32_t)lb;
+                d[5] = (int32_t)mx;
+                d[6] = (int32_t)neq_row;
+            }
+        }
+#endif
         wave_lds_fence();  // the previous group's winners are no longer read
         for (int p = k + q; p < k4; p += 16) {
             wkey[p] = 0u;
@@ -450,6 +487,19 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
             }
         }
         wave_lds_fence();
+#if MAXK_TOPK_DIAG == 3  // tools only: the row's LDS winner region and per-lane slot state,
+                         // into its dense output row (call maxk_topk_cbsr_dense)
+        if (out_dense && live) {
+            uint32_t *dr = reinterpret_cast<uint32_t *>(out_dense + (int64_t)row * D);
+            for (int w = q; w < 3 * k4 && w < 160; w += 16) dr[w] = wkey[w];
+            dr[160 + q] = row_prefix_excl(nw);
+            dr[176 + q] = nw;
+            dr[192 + q] = (uint32_t)(wkey - lds_topk);
+            dr[208 + q] = (uint32_t)(wcol - lds_topk);
+            dr[224 + q] = slot;
+        }
+        wave_lds_fence();
+#endif
         if (live) {
             for (int p = q; p < k; p += 16) {
                 const uint32_t kp = wkey[p], cp = wcol[p];
@@ -469,13 +519,20 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
                 else
                     out_val[o] = (T)vb;
                 out_idx[o] = (uint8_t)cp;
-                if (out_idx32) out_idx32[o] = (int32_t)cp;
+                if (out_idx32 && !MAXK_TOPK_DIAG) out_idx32[o] = (int32_t)cp;
+#if MAXK_TOPK_DIAG == 2  // tools only: per LDS slot p, column | rank << 8 | key low 16 << 16
+                if (out_idx32) out_idx32[(int64_t)row * k + p] =
+                    (int32_t)(cp | ((uint32_t)pos << 8) | (kp << 16));
+#endif
             }
         }
         wave_lds_fence();  // winners read before the next group's histogram overwrites them
     }
 }
 
+#ifdef wave_lds_fence
+#undef wave_lds_fence
+#endif
 // dense[r, :] = 0; dense[r, idx[r, l]] = val[r, l] + add[r, idx[r, l]]   (val and add
 // optional).  One wave per row, grid-stride: one workgroup per 4 rows would be bound by
 // workgroup dispatch on large graphs.  A row's reads all land in LDS before its stores, so
@@ -566,7 +623,8 @@ int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, 
     MAXK_REQUIRE(ld_x >= D, "ld_x (%lld) < dim_origin (%d)", (long long)ld_x, D);
     if (num_rows == 0) return MAXK_OK;
     MAXK_REQUIRE(x && val && idx, "x/val/idx must not be NULL");
-    if (MAXK_TOPK_ROWS4 && k <= 32) {  // past k=32 its k^2 ranking loses to one row per wave
+    if (MAXK_TOPK_ROWS4 && k <= MAXK_TOPK_ROWS4_KMAX) {  // at k=64 its k^2 ranking ties one
+                                                         // row per wave
         const int k4 = (k + 3) & ~3;
         const int words = 4 * 3 * k4;  // per wave: 4 rows of winners (key, value, column)
         const size_t lds = (size_t)kWavesPerBlock * words * 4;
@@ -574,14 +632,15 @@ int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, 
                          (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(T))) == 0;
         const int64_t blocks = ceil_div(num_rows, 4 * kWavesPerBlock);
         const dim3 grid((unsigned)(blocks < MAXK_TOPK_BLOCKS ? blocks : MAXK_TOPK_BLOCKS));
-        if (vec)
-            hipLaunchKernelGGL((topk_rows4_kernel<T, true>), grid, dim3(kBlock), lds,
-                               as_stream(stream), x, ld_x, val, idx, idx32, dense, (int)num_rows, D,
-                               k, words);
+        // J = lane keys kept for the lower bound: 2 up to k = 32, 4 up to 64
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, grid, dim3(kBlock), lds, as_stream(stream), x, ld_x, val, idx,
+                               idx32, dense, (int)num_rows, D, k, words);
+        };
+        if (k <= 32)
+            vec ? go(topk_rows4_kernel<T, true, 2>) : go(topk_rows4_kernel<T, false, 2>);
         else
-            hipLaunchKernelGGL((topk_rows4_kernel<T, false>), grid, dim3(kBlock), lds,
-                               as_stream(stream), x, ld_x, val, idx, idx32, dense, (int)num_rows, D,
-                               k, words);
+            vec ? go(topk_rows4_kernel<T, true, 4>) : go(topk_rows4_kernel<T, false, 4>);
         MAXK_LAUNCHED("topk_rows4_kernel");
         return MAXK_OK;
     }

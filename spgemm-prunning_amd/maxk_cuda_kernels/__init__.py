@@ -313,7 +313,8 @@ _PULL_CACHE: dict = {}
 
 
 def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_cols: int,
-              k: int, dim: int = 256, slices: Optional[int] = None, cache: bool = True):
+              k: int, dim: int = 256, slices: Optional[int] = None, cache: bool = True,
+              shift: Optional[int] = None):
     """(tile_ptr int32 [S*nb+1], ent int32 [E, 2], shift, S) of a CSR graph and its edge
     values for the pull backward at width k: rows cut into S slices (default
     maxk_pull_slices: ~3.5 MiB of G rows per slice and rank part, at most 3 parts), columns into
@@ -322,12 +323,13 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     << 16, weight bits}.  Built on the GPU (one stable radix sort); cached per
     (indptr, indices, values) tensor objects and their version counters -- indptr assigns
     the edges to rows and slices, and the weights are copied into the plan, so a plan serves
-    the graph and values it was built from."""
+    the graph and values it was built from.  `shift` overrides the bucket shift
+    (maxk_pull_shift(k) by default; any shift the C ABI accepts for k)."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32)):
         _need(t, n, dt)
     L = _lib()
-    shift = int(L.maxk_pull_shift(int(k)))
+    shift = int(L.maxk_pull_shift(int(k))) if shift is None else int(shift)
     if shift < 0:
         raise RuntimeError(f"pull_plan: invalid k {k}")
     num_rows = indptr.numel() - 1

@@ -29,6 +29,7 @@ SIGNATURES = {
     "maxk_last_error": (ctypes.c_char_p, []),
     "maxk_device_count": (ctypes.c_int, []),
     "maxk_source_digest": (ctypes.c_char_p, []),
+    "maxk_build_config": (ctypes.c_char_p, []),
     "maxk_spgemm_forward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_spgemm_forward": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),

@@ -146,6 +146,28 @@ def test_pull_plan_follows_values(mk, cuda):
     close(c, a.cpu().numpy())
 
 
+@pytest.mark.parametrize("k", [8, 16, 32, 64])
+def test_pull_backward_other_shifts(mk, cuda, k):
+    """A pull plan built with a bucket shift other than maxk_pull_shift(k) (any shift in
+    [4, max(maxk_bucket_shift, maxk_pull_shift)]) runs in a workspace of the documented size
+    (maxk_sspmm_backward_pull_workspace_size) -- ADVICE r02: the call used to size its tile
+    partials at the largest shift and refuse the documented workspace."""
+    z = load_golden(next(c for c in CASES if "sym_d256_k16" in c))
+    V = z["row_ptr"].size - 1
+    rng = np.random.default_rng(k)
+    sel = np.stack([rng.choice(256, k, replace=False) for _ in range(V)]).astype(np.uint8)
+    g = rng.standard_normal((V, 256), dtype=np.float32)
+    args = [T(z[n], cuda) for n in ("row_ptr", "col_idx", "val")]
+    ref = O.sspmm_bwd(z["row_ptr"], z["col_idx"], z["val"], g, sel, row_div=z["deg"])
+    L = mk._lib()
+    top = max(L.maxk_bucket_shift(k), L.maxk_pull_shift(k))
+    for shift in sorted({4, L.maxk_bucket_shift(k), L.maxk_pull_shift(k), top - 1}):
+        plan = mk.pull_plan(*args, V, k, 256, slices=3, cache=False, shift=shift)
+        gs = mk.sspmm_backward(*args, T(g, cuda), T(sel, cuda), row_div=T(z["deg"], cuda),
+                               mode="pull", plan=plan)
+        close(gs, ref)
+
+
 def test_pull_backward_repeats(mk, cuda):
     """fp64 tile sums, slices added in a fixed order: two runs agree to fp32 rounding."""
     z = load_golden(CASES[2])
