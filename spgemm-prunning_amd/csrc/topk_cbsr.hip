@@ -351,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
             // Gaussian row's does: 0x3F7F... -> 0x4000...); the count of keys >= mid == k
             // ends a row early in both.
             uint32_t lo = lb, hi = mx;
-            bool done = !live || lo == hi;
+            bool done = lo == hi;  // rows past the end search too (see `take` below)
             for (;;) {
                 const bool go = !done;
                 if (__ballot(go) == 0) break;
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
             int bit = diff ? 31 - __builtin_clz(diff) : -1;
             // common prefix of the keys (all keys are >= it); bit 31 differing -> no prefix
             thr = !diff ? mx : (bit == 31 ? 0u : mx & (~0u << (bit + 1)));
-            bool done = !live || diff == 0u;
+            bool done = diff == 0u;
             for (;;) {
                 const bool go = !done && bit >= 0;
                 if (__ballot(go) == 0) break;
@@ -403,16 +403,18 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
 #pragma unroll
         for (int t = 0; t < 16; ++t) neq += (ok[t] && (key[t] >> sh) == T_) ? 1u : 0u;
         const uint32_t neq_row = row_sum(neq);  // every lane: DPP reads the whole row
-        const bool ties = live && neq_row != (uint32_t)need;
-        // A row past the end (the last row group's dead sub-rows) takes nothing: its search
-        // never ran (thr = its lower bound), so "key >= thr" would take 32-100 winners and
-        // its compaction would run past its 3*k4 LDS words into the next wave's winners --
-        // which that wave, one grid-stride round behind, may still be ranking (r02's k = 48
-        // mismatch: row 2186888 of the seed-0 [2449029, 256] Gaussian input).
+        // Rows past the end (the last row group's dead sub-rows, holding a copy of the last
+        // row) run the same exact search and take exactly k winners; they only skip the
+        // stores.  Skipping their search (r02) left thr at their lower bound, so "key >= thr"
+        // took 32-100 winners whose compaction ran past the row's 3*k4 LDS words into the next
+        // wave's winners -- which that wave, one grid-stride round behind, could still be
+        // ranking (r02's k = 48 mismatch on row 2186888 of the seed-0 [2449029, 256] Gaussian
+        // input).  Searching costs nothing there; a `live` test per key cost 2-3 %.
+        const bool ties = neq_row != (uint32_t)need;
         bool take[16];
         if (__ballot(ties) == 0) {
 #pragma unroll
-            for (int t = 0; t < 16; ++t) take[t] = live && ok[t] && (key[t] >> sh) >= T_;
+            for (int t = 0; t < 16; ++t) take[t] = ok[t] && (key[t] >> sh) >= T_;
         } else {  // rank the equal keys in column order: chunk i, then lane, then j
             uint32_t base = 0;
 #pragma unroll
@@ -425,7 +427,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
                 for (int j = 0; j < 4; ++j) {
                     const int t = 4 * i + j;
                     const bool eq = ok[t] && (key[t] >> sh) == T_;
-                    take[t] = live && ((ok[t] && (key[t] >> sh) > T_) || (eq && r < (uint32_t)need));
+                    take[t] = (ok[t] && (key[t] >> sh) > T_) || (eq && r < (uint32_t)need);
                     r += eq ? 1u : 0u;
                 }
                 base += row_sum(c);

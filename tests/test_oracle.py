@@ -81,3 +81,18 @@ def test_oracle_row_range_sample():
                         rows=(10, 50))
     assert np.array_equal(part[10:50], full[10:50])
     assert not part[:10].any() and not part[50:].any()
+
+
+def test_topk_tail_fixture_pins_the_oracle():
+    """tests/golden/topk/topk_tail_overflow.npz (tools/make_topk_tail_fixture.py): the rows of
+    the seed-0 Gaussian input behind r02's four-row k=48 mismatch, with their top-k as the
+    oracle computed them on the box; the oracle here reproduces them bit for bit, and they
+    agree with numpy's stable descending sort (ties to the lower column)."""
+    import os
+    from conftest import GOLDEN
+    z = load_golden(os.path.join(GOLDEN, "topk", "topk_tail_overflow.npz"))
+    for k in (16, 32, 48, 64):
+        v, i = O.topk(z["x"], k)
+        assert np.array_equal(v, z[f"val_k{k}"]) and np.array_equal(i, z[f"idx_k{k}"])
+        order = np.argsort(-z["x"], axis=1, kind="stable")[:, :k]
+        assert np.array_equal(order.astype(np.uint8), i)
