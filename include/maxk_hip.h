@@ -231,6 +231,75 @@ int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *
                    size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Hybrid backward and the "auto" backward rule through the C ABI (the Python binding's
+ * hybrid_plan / pull_locality / _bwd_mode / _scaled_entries, maxk_cuda_kernels/__init__.py,
+ * rest on these).  Replaces the same reference kernels as maxk_sspmm_backward
+ * (spmm_maxk_backward.cu:15-121, launched by cuda_kernel_wrappers.cu:58-76).
+ *
+ * maxk_backward_mode_auto: the backward a graph should use (pure host arithmetic):
+ *   MAXK_BWD_PULL where dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and the graph has at
+ *   least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(dim_k) columns) or a G of at
+ *   most 64 MiB; else MAXK_BWD_BUCKET on such a dense graph at dim_k <= 16; else MAXK_BWD_HYBRID
+ *   when pull_locality (maxk_pull_locality at maxk_pull_shift(dim_k); < 0 = unknown) reaches
+ *   MAXK_HYBRID_LOCALITY and dim_k % 4 == 0; else MAXK_BWD_CSC.
+ * maxk_pull_locality (synchronous): num_e / occupied (source row, bucket of 2^bucket_shift
+ *   columns) pairs, columns sorted within rows; workspace >= 8 bytes.
+ * maxk_hybrid_plan (synchronous): from the graph's pull plan (maxk_pull_plan with bucket_shift,
+ *   slices), the tiles holding at least density x (rows of their slice) entries --
+ *   tile_list[S*nb] (increasing tile ids), tile_ent[S*nb+1] (their runs in ent_pull[2*num_e]),
+ *   bucket_ptr[nb+1] / bucket_tiles[S*nb] (per bucket, positions in tile_list in slice order)
+ *   -- and every other edge as a CSR off_row_ptr[num_rows+1] / off_col[num_e] / off_val[num_e]
+ *   (CSR order kept).  counts[3] = {tiles pulled, entries pulled, edges off}.  Buffers are
+ *   sized for the worst case; the counts say how much of each holds the plan.
+ * maxk_pull_entries_scale: ent_out = ent with each weight divided by its source row's
+ *   row_div, for n_runs tile runs (tile_ids[i], or i when NULL; entries tile_ent[i] ..
+ *   tile_ent[i+1]) -- once per (plan, divisor), so the pull gathers G instead of G / row_div.
+ * maxk_sspmm_backward_hybrid: the csc backward over the off-tile CSR (its transpose plan:
+ *   maxk_transpose_plan of off_col) and the listed-tile pull over the rest, accumulated into
+ *   grad_cbsr.  With side_stream (and two caller-created events ev_fork / ev_join, as void*)
+ *   the tile kernels run beside the csc and are joined before the final reduce; NULL runs
+ *   everything on `stream`.  flags: MAXK_HYBRID_PRESCALED when ent_pull carries row_div.
+ * ------------------------------------------------------------------------- */
+#define MAXK_BWD_PULL 0
+#define MAXK_BWD_CSC 1
+#define MAXK_BWD_BUCKET 2
+#define MAXK_BWD_HYBRID 3
+#define MAXK_BWD_ATOMIC 4
+#define MAXK_HYBRID_LOCALITY 1.5
+#define MAXK_HYBRID_DENSITY 0.5f
+#define MAXK_HYBRID_PRESCALED 1
+int maxk_backward_mode_auto(int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                            int32_t dim_k, double pull_locality);
+int maxk_pull_locality(const int32_t *row_ptr, const int32_t *col_idx, int64_t num_rows,
+                       int64_t num_e, int32_t bucket_shift, double *locality, void *workspace,
+                       size_t workspace_bytes, void *stream);
+size_t maxk_hybrid_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                       int32_t bucket_shift, int32_t slices);
+int maxk_hybrid_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                     const int32_t *tile_ptr, const uint32_t *ent, int64_t num_rows,
+                     int64_t num_cols, int64_t num_e, int32_t bucket_shift, int32_t slices,
+                     float density, int32_t *tile_list, int32_t *tile_ent, int32_t *bucket_ptr,
+                     int32_t *bucket_tiles, uint32_t *ent_pull, int32_t *off_row_ptr,
+                     int32_t *off_col, float *off_val, int64_t *counts, void *workspace,
+                     size_t workspace_bytes, void *stream);
+int maxk_pull_entries_scale(const uint32_t *ent, const int32_t *tile_ids, const int32_t *tile_ent,
+                            int64_t n_runs, int64_t num_rows, int64_t num_cols,
+                            int32_t bucket_shift, int32_t slices, const float *row_div,
+                            uint32_t *ent_out, void *stream);
+size_t maxk_sspmm_backward_hybrid_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                 int64_t n_off_e, int32_t dim_origin,
+                                                 int32_t dim_k, int64_t n_tiles);
+int maxk_sspmm_backward_hybrid(
+    const float *grad_out, const float *row_div, const uint8_t *cbsr_idx,
+    const int32_t *tile_list, const int32_t *tile_ent, int32_t n_tiles, const int32_t *bucket_ptr,
+    const int32_t *bucket_tiles, const uint32_t *ent_pull, int64_t n_pull_e, int32_t bucket_shift,
+    int32_t slices, const int32_t *off_row_ptr, const int32_t *off_col, const float *off_val,
+    int64_t n_off_e, const int32_t *off_col_ptr, const int32_t *off_csc_eid, int32_t flags,
+    float *grad_cbsr, int64_t num_rows, int64_t num_cols, int32_t dim_origin, int32_t dim_k,
+    void *workspace, size_t workspace_bytes, void *stream, void *side_stream, void *ev_fork,
+    void *ev_join);
+
+/* ---------------------------------------------------------------------------
  * CBSR encode (MaxK top-k): per row the k largest of dim_origin values, in
  * torch.topk(largest=True, sorted=True) order (value descending; NaN largest;
  * equal values by ascending column).  x has leading dimension ld_x (elements).

@@ -366,6 +366,9 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
 
 _HYBRID_CACHE: "dict" = {}
 MAXK_PULL_NO_REDUCE, MAXK_PULL_REDUCE_ONLY = 2, 4  # include/maxk_hip.h
+MAXK_HYBRID_PRESCALED = 1
+# maxk_backward_mode_auto's codes (include/maxk_hip.h MAXK_BWD_*)
+_MODE_OF_CODE = {0: "pull", 1: "csc", 2: "bucket", 3: "hybrid", 4: "atomic"}
 _SIDE: "dict" = {}
 
 
@@ -376,23 +379,23 @@ def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
         _SIDE[i] = torch.cuda.Stream(device=i)
     return _SIDE[i]
 # a tile pulls when it holds at least this many entries per row of its slice
-HYBRID_DENSITY = 0.5
+HYBRID_DENSITY = 0.5  # MAXK_HYBRID_DENSITY in include/maxk_hip.h
 # mode "auto" picks "hybrid" on a sparse graph whose pull_locality reaches this (products-
 # sized, k=32: 1.02 (random labels) csc 8.2 vs hybrid 8.4 ms; 1.9: 8.1 vs 6.4; 6.9: 7.4 vs 4.7)
-HYBRID_LOCALITY = 1.5
+HYBRID_LOCALITY = 1.5  # MAXK_HYBRID_LOCALITY
 
 
 def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
                 num_cols: int, k: int, dim: int = 256, density: Optional[float] = None,
                 cache: bool = True):
-    """Plan of the "hybrid" backward: the pull over the dense tiles of the graph's pull plan
-    (at least `density` entries per row of the tile's slice), the two-phase csc over the other
-    edges.  A community-ordered graph keeps most edges in the tiles near the diagonal, which
-    pull well, while a pull over every tile would write one [num_cols, k] partial per row
-    slice (maxk_sspmm_backward_pull_tiles in include/maxk_hip.h).  Returns (tile_list,
-    tile_ent, bucket_ptr, bucket_tiles, ent, shift, S, (off_indptr, off_indices, off_values,
-    off_transpose_plan)); cached like pull_plan.  k % 4 == 0.  `density` defaults to
-    MAXK_HYBRID_DENSITY or HYBRID_DENSITY."""
+    """Plan of the "hybrid" backward (maxk_hybrid_plan, C ABI): the pull over the dense tiles
+    of the graph's pull plan (at least `density` entries per row of the tile's slice), the
+    two-phase csc over the other edges.  A community-ordered graph keeps most edges in the
+    tiles near the diagonal, which pull well, while a pull over every tile would write one
+    [num_cols, k] partial per row slice.  Returns (tile_list, tile_ent, bucket_ptr,
+    bucket_tiles, ent, shift, S, (off_indptr, off_indices, off_values, off_transpose_plan));
+    cached like pull_plan.  k % 4 == 0.  `density` defaults to MAXK_HYBRID_DENSITY or
+    HYBRID_DENSITY."""
     if density is None:
         density = float(os.environ.get("MAXK_HYBRID_DENSITY", HYBRID_DENSITY))
     if k % 4:
@@ -407,40 +410,38 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
             return plan
     tptr, ent, shift, S = pull_plan(indptr, indices, values, num_cols, k, dim, cache=False)
     dev = indices.device
+    L = _lib()
     num_rows = indptr.numel() - 1
-    nb = int(_lib().maxk_bucket_count(num_cols, shift))
-    rps = -(-num_rows // S)
-    cnt = torch.diff(tptr.long())
-    t_all = torch.arange(S * nb, device=dev)
-    rows_in = torch.clamp(num_rows - (t_all // nb) * rps, max=rps).clamp(min=1)
-    dense = (cnt > 0) & (cnt >= density * rows_in)
-    t_of = torch.repeat_interleave(t_all, cnt)
-    keep = dense[t_of]
-    tile_list = torch.nonzero(dense).flatten()
-    tile_ent = torch.zeros(tile_list.numel() + 1, dtype=torch.int64, device=dev)
-    tile_ent[1:] = torch.cumsum(cnt[tile_list], 0)
-    j = tile_list % nb
-    order = torch.argsort(j * S + tile_list // nb)
-    bucket_ptr = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
-    bucket_ptr[1:] = torch.cumsum(torch.bincount(j, minlength=nb), 0)
-    ent_d = ent[keep].contiguous()
-    # the other edges back to a CSR (rows, then columns), with their weights
-    eo = ent[~keep]
-    to = t_of[~keep]
-    x = eo[:, 0].long() & 0xffffffff
-    rows = (to // nb) * rps + (x & 0xffff)
-    cols = ((to % nb) << shift) + (x >> 16)
-    vals = eo[:, 1].contiguous().view(torch.float32)
-    srt = torch.argsort(rows * num_cols + cols)
-    off_ip = torch.zeros(num_rows + 1, dtype=torch.int64, device=dev)
-    off_ip[1:] = torch.cumsum(torch.bincount(rows, minlength=num_rows), 0)
-    off_ix = cols[srt].to(torch.int32).contiguous()
-    off_val = vals[srt].contiguous()
-    off_ip = off_ip.to(torch.int32)
+    E = indices.numel()
+    nb = int(L.maxk_bucket_count(num_cols, shift))
+    nt = S * nb
+    i32 = dict(dtype=torch.int32, device=dev)
+    tile_list = torch.empty(max(nt, 1), **i32)
+    tile_ent = torch.empty(nt + 1, **i32)
+    bucket_ptr = torch.empty(nb + 1, **i32)
+    bucket_tiles = torch.empty(max(nt, 1), **i32)
+    ent_d = torch.empty(max(E, 1), 2, **i32)
+    off_ip = torch.empty(num_rows + 1, **i32)
+    off_ix = torch.empty(max(E, 1), **i32)
+    off_val = torch.empty(max(E, 1), dtype=torch.float32, device=dev)
+    ws = torch.empty(max(1, L.maxk_hybrid_plan_workspace_size(num_rows, num_cols, E, shift, S)),
+                     dtype=torch.uint8, device=dev)
+    counts = (ctypes.c_int64 * 3)()
+    with torch.cuda.device(dev):
+        _capi.check(L.maxk_hybrid_plan(
+            _ptr(indptr), _ptr(indices), _ptr(values), _ptr(tptr), _ptr(ent), num_rows, num_cols,
+            E, shift, S, float(density), _ptr(tile_list), _ptr(tile_ent), _ptr(bucket_ptr),
+            _ptr(bucket_tiles), _ptr(ent_d), _ptr(off_ip), _ptr(off_ix), _ptr(off_val), counts,
+            _ptr(ws), ws.numel(), _stream(dev)), "maxk_hybrid_plan")
+    n_t, n_p, n_o = (int(c) for c in counts)
+    del tptr, ent, ws
+    # the slices are views of their worst-case buffers; copies keep the plan compact
+    tile_list, bucket_tiles = tile_list[:n_t].clone(), bucket_tiles[:n_t].clone()
+    tile_ent = tile_ent[:n_t + 1].clone()
+    ent_d = ent_d[:n_p].clone()
+    off_ix, off_val = off_ix[:n_o].clone(), off_val[:n_o].clone()
     off = (off_ip, off_ix, off_val, transpose_plan(off_ix, num_cols, cache=False))
-    i32 = lambda t: t.to(torch.int32).contiguous()  # noqa: E731
-    plan = (i32(tile_list), i32(tile_ent), i32(bucket_ptr), i32(order), ent_d, shift, S, off)
-    del tptr, ent, cnt, t_all, rows_in, t_of, keep, eo, to, x, rows, cols, vals, srt
+    plan = (tile_list, tile_ent, bucket_ptr, bucket_tiles, ent_d, shift, S, off)
     if cache:
         if key not in _HYBRID_CACHE:
             for t in (indptr, indices, values):
@@ -460,14 +461,16 @@ _LOCALITY: "dict" = {}
 _SCALED: "dict" = {}
 
 
-def _scaled_entries(ent: torch.Tensor, tiles: torch.Tensor, counts: torch.Tensor, nb: int,
-                    rps: int, row_div: torch.Tensor) -> torch.Tensor:
-    """The pull entries with each weight divided by its source row's row_div, so the tile
-    kernels gather G itself instead of a G / row_div copy (gprime_kernel: a read and a write
-    of all of G per call; ogbn-products 2 x 2.5 GB).  `tiles[i]` is the tile of the entries'
-    i-th run of `counts[i]`.  Cached per entry tensor for one (row_div object, version): the
-    degrees a layer divides by are the same tensor every call (maxk_layers.CSRGraph).  None
-    when it would have to be built inside a stream capture."""
+def _scaled_entries(ent: torch.Tensor, tiles: Optional[torch.Tensor], tile_ent: torch.Tensor,
+                    num_rows: int, num_cols: int, shift: int, S: int,
+                    row_div: torch.Tensor) -> Optional[torch.Tensor]:
+    """The pull entries with each weight divided by its source row's row_div
+    (maxk_pull_entries_scale), so the tile kernels gather G itself instead of a G / row_div
+    copy (gprime_kernel: a read and a write of all of G per call; ogbn-products 2 x 2.5 GB).
+    `tiles[i]` (None: i) is the tile of the entries' i-th run [tile_ent[i], tile_ent[i+1]).
+    Cached per entry tensor for one (row_div object, version): the degrees a layer divides by
+    are the same tensor every call (maxk_layers.CSRGraph).  None when it would have to be built
+    inside a stream capture."""
     key = id(ent)
     hit = _SCALED.get(key)
     if hit is not None:
@@ -478,12 +481,13 @@ def _scaled_entries(ent: torch.Tensor, tiles: torch.Tensor, counts: torch.Tensor
         # a hipGraph capture records kernels without running them: a copy built here would
         # be cached before it holds anything, so the caller keeps the G / row_div route
         return None
-    t = torch.repeat_interleave(tiles.long(), counts.long())
-    rows = (t // nb) * rps + (ent[:, 0].long() & 0xffff)
-    del t
-    sc = ent.clone()
-    sc[:, 1] = (ent[:, 1].view(torch.float32) / row_div[rows]).view(torch.int32)
-    del rows
+    sc = torch.empty_like(ent)
+    dev = ent.device
+    n_runs = tile_ent.numel() - 1
+    with torch.cuda.device(dev):
+        _capi.check(_lib().maxk_pull_entries_scale(
+            _ptr(ent), _ptr(tiles), _ptr(tile_ent), n_runs, num_rows, num_cols, shift, S,
+            _ptr(row_div), _ptr(sc), _stream(dev)), "maxk_pull_entries_scale")
     if key not in _SCALED:
         weakref.finalize(ent, _SCALED.pop, key, None)
     _SCALED[key] = (weakref.ref(ent), weakref.ref(row_div), row_div._version, sc)
@@ -496,13 +500,13 @@ def _prescale() -> bool:
 
 
 def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> float:
-    """Edges per occupied (source row, bucket of 2^shift columns) pair: how many entries of
-    a pull tile share a source row's G lines.  A randomly labelled graph with `a` edges per
-    (row, bucket) on average has a / (1 - e^-a) (ogbn-products-sized: ~1.0); a graph whose
-    vertex order groups its communities (maxk_graph.locality_order) has many more, whatever
-    the average.  One pass over the edges (columns sorted within rows, else an under-
-    estimate), cached per (indptr, indices, shift) and their versions.  Reported by bench.py
-    (extra.pull_locality); on sparse graphs it steers mode "auto" to "hybrid" (_bwd_mode)."""
+    """Edges per occupied (source row, bucket of 2^shift columns) pair (maxk_pull_locality):
+    how many entries of a pull tile share a source row's G lines.  A randomly labelled graph
+    with `a` edges per (row, bucket) on average has a / (1 - e^-a) (ogbn-products-sized:
+    ~1.0); a graph whose vertex order groups its communities (maxk_graph.locality_order) has
+    many more, whatever the average.  One pass over the edges (columns sorted within rows,
+    else an under-estimate), cached per (indptr, indices, shift) and their versions.  Reported
+    by bench.py (extra.pull_locality); on sparse graphs it steers mode "auto" to "hybrid"."""
     key = (id(indptr), id(indices), int(shift))
     hit = _LOCALITY.get(key)
     if hit is not None:
@@ -510,17 +514,17 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
         if rp() is indptr and ri() is indices and pv == indptr._version and \
                 iv == indices._version:
             return val
-    E = indices.numel()
-    if E == 0:
-        val = 0.0
-    else:
-        b = indices.long() >> int(shift)
-        new = torch.ones(E, dtype=torch.bool, device=indices.device)
-        new[1:] = b[1:] != b[:-1]
-        starts = indptr[:-1].long()
-        new[starts[starts < E]] = True  # a row's first edge opens a pair
-        val = E / max(1, int(new.sum()))
-        del b, new
+    _need(indptr, "indptr", torch.int32)
+    _need(indices, "indices", torch.int32)
+    dev = indices.device
+    out = ctypes.c_double(0.0)
+    ws = torch.empty(8, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(_lib().maxk_pull_locality(_ptr(indptr), _ptr(indices), indptr.numel() - 1,
+                                              indices.numel(), int(shift), ctypes.byref(out),
+                                              _ptr(ws), ws.numel(), _stream(dev)),
+                    "maxk_pull_locality")
+    val = float(out.value)
     if key not in _LOCALITY:
         weakref.finalize(indices, _LOCALITY.pop, key, None)
     _LOCALITY[key] = (weakref.ref(indptr), weakref.ref(indices), indptr._version,
@@ -531,37 +535,33 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
 def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0,
               num_rows: Optional[int] = None, dim: Optional[int] = None,
               graph: Optional[tuple] = None) -> str:
-    """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) picks "pull"
-    where it measured faster than "csc": k % 4 == 0 or k <= 64, dim % 4 == 0 when dim is
-    given, and at
-    least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(k) columns) on average
-    (Reddit k=16: 2.2, k=64: 0.54; ogbn-proteins k=64: 1.2; ogbn-products: 0.02), or a
-    gradient G of at most 64 MiB (num_rows x dim x 4 B; Flickr: 23 MB, 0.05 vs 0.13 ms), which
-    stays cache-resident however sparse the graph; for more than 256 x 65536 rows "bucket"
-    (k <= 16) stands in.  On a sparse graph the whole pull loses even with locality (its
-    per-slice partials, [num_cols, k] per row slice: a community-ordered ogbn-products-sized
-    graph 46 ms against 8 ms csc), but where `graph` = (indptr, indices) is
-    given and its pull_locality reaches HYBRID_LOCALITY (k % 4 == 0, dim % 4 == 0) "hybrid"
-    pulls the dense tiles and runs csc over the rest (that graph: 4.7 against 7.4 ms).
-    "bucket" (two-phase with the same fp64 accumulator) stays selectable."""
+    """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) is the C ABI's
+    rule, maxk_backward_mode_auto: "pull" where it measured faster than "csc" -- k % 4 == 0
+    or k <= 64, dim % 4 == 0 when dim is given, and at least ~1/2 edge per (source row,
+    bucket of 2^maxk_bucket_shift(k) columns) on average (Reddit k=16: 2.2, k=64: 0.54;
+    ogbn-proteins k=64: 1.2; ogbn-products: 0.02), or a gradient G of at most 64 MiB (Flickr:
+    23 MB, 0.05 vs 0.13 ms), which stays cache-resident however sparse the graph; for more
+    than 256 x 65536 rows "bucket" (k <= 16) stands in.  On a sparse graph the whole pull loses
+    even with locality (its per-slice partials, [num_cols, k] per row slice: a community-
+    ordered ogbn-products-sized graph 46 ms against 8 ms csc), but where
+    `graph` = (indptr, indices) is given and its pull_locality reaches HYBRID_LOCALITY (k % 4
+    == 0, dim % 4 == 0) "hybrid" pulls the dense tiles and runs csc over the rest (that graph:
+    4.7 against 7.4 ms).  "pull", "bucket" and "hybrid" sum in fp64 LDS accumulators: two runs
+    agree except in rare fp32 rounding ties; MAXK_BWD_MODE=csc forces the bitwise-
+    deterministic form everywhere."""
     mode = mode or os.environ.get("MAXK_BWD_MODE", "auto")
     if mode not in BWD_MODES:
         raise RuntimeError(f"backward mode must be one of {BWD_MODES}, got {mode!r}")
     if mode == "auto":
-        mode = "csc"
-        if (k % 4 == 0 or k <= 64) and num_cols > 0 and (dim is None or dim % 4 == 0):
-            shift = int(_lib().maxk_bucket_shift(int(k)))
-            rows = num_rows if num_rows else num_cols
-            dense = num_e * (1 << shift) >= rows * num_cols // 2
-            small = dim is not None and rows * dim * 4 <= (64 << 20)
-            if (dense or small) and rows <= 256 * 65536:
-                mode = "pull"
-            elif dense and k <= 16 and k % 4 == 0:
-                mode = "bucket"
-            elif (graph is not None and k % 4 == 0 and rows <= 256 * 65536 and num_e > 0
-                  and pull_locality(graph[0], graph[1], int(_lib().maxk_pull_shift(int(k))))
-                  >= HYBRID_LOCALITY):
-                mode = "hybrid"
+        L = _lib()
+        rows = num_rows if num_rows else num_cols
+        D = -1 if dim is None else int(dim)
+        code = int(L.maxk_backward_mode_auto(rows, num_cols, num_e, D, int(k), -1.0))
+        if (code == 1 and graph is not None and k % 4 == 0 and num_e > 0
+                and rows <= 256 * 65536):  # csc unless the graph's locality asks for hybrid
+            loc = pull_locality(graph[0], graph[1], int(L.maxk_pull_shift(int(k))))
+            code = int(L.maxk_backward_mode_auto(rows, num_cols, num_e, D, int(k), loc))
+        mode = _MODE_OF_CODE[code]
     if mode == "bucket" and k % 4 != 0:
         raise RuntimeError(f"backward mode 'bucket' needs k % 4 == 0, got k={k}")
     if mode == "pull" and k % 4 != 0 and k > 64:
@@ -644,51 +644,59 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     if mode == "hybrid":
         tl, te, bp, bt, ent, shift, S, off = (plan if plan is not None else
                                              hybrid_plan(indptr, indices, values, num_cols, k, D))
-        oip, oix, oval, otp = off
+        oip, oix, oval, (ocp, oeid) = off
         n_t = tl.numel()
-        ws_bytes = L.maxk_sspmm_backward_pull_tiles_workspace_size(num_rows, num_cols, D, k, n_t)
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-
-        pdiv = row_div
+        flags = 0
         if row_div is not None and n_t > 0 and _prescale():
-            sc = _scaled_entries(ent, tl, torch.diff(te), int(L.maxk_bucket_count(num_cols, shift)),
-                                 -(-num_rows // S), row_div)
+            sc = _scaled_entries(ent, tl, te, num_rows, num_cols, shift, S, row_div)
             if sc is not None:
-                ent, pdiv = sc, None
-
-        def tiles(flags):
-            _capi.check(L.maxk_sspmm_backward_pull_tiles(
-                _ptr(grad_output), _ptr(pdiv), _ptr(cbsr_idx), _ptr(tl), _ptr(te), n_t,
-                _ptr(bp), _ptr(bt), _ptr(ent), shift, S, flags, _ptr(out), num_rows, num_cols,
-                ent.shape[0], D, k, _ptr(ws), ws.numel(), _stream(dev)),
-                "maxk_sspmm_backward_pull_tiles")
+                ent, flags = sc, MAXK_HYBRID_PRESCALED
+        ws_bytes = L.maxk_sspmm_backward_hybrid_workspace_size(num_rows, num_cols, oix.numel(),
+                                                               D, k, n_t)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         with torch.cuda.device(dev):
             overlap = (oix.numel() > 0 and n_t > 0
                        and os.environ.get("MAXK_HYBRID_STREAMS", "1") != "0")
-            if overlap:  # the tile kernels on a side stream beside the csc, joined at the reduce
-                main = torch.cuda.current_stream(dev)
-                side = _side_stream(dev)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    tiles(MAXK_PULL_NO_REDUCE)
-            if oix.numel():  # the sparse tiles' edges: two-phase csc, into out
-                sspmm_backward(oip, oix, oval, grad_output, cbsr_idx, row_div=row_div,
-                               chunk=chunk, out=out, validate=False, mode="csc", plan=otp)
-            else:
-                out.zero_()
-            if overlap:
-                main.wait_stream(side)
-                tiles(MAXK_PULL_REDUCE_ONLY | 1)
-            else:
-                tiles(1)
+            if not overlap:  # everything on the caller's stream, in one C-ABI call
+                _capi.check(L.maxk_sspmm_backward_hybrid(
+                    _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tl), _ptr(te), n_t,
+                    _ptr(bp), _ptr(bt), _ptr(ent), ent.shape[0], shift, S, _ptr(oip), _ptr(oix),
+                    _ptr(oval), oix.numel(), _ptr(ocp), _ptr(oeid), flags, _ptr(out), num_rows,
+                    num_cols, D, k, _ptr(ws), ws.numel(), _stream(dev), None, None, None),
+                    "maxk_sspmm_backward_hybrid")
+                return out
+            # the same sequence with the tile kernels on a side stream beside the csc, forked
+            # and joined by torch (fresh events each call: one pair re-recorded by eager calls
+            # broke the join of a graph captured with it, test_hipgraph_capture_*[hybrid])
+            a = L.maxk_sspmm_backward_csc_workspace_size(num_rows, num_cols, oix.numel(), D, k, 0)
+            a = (a + 255) // 256 * 256
+            ws_csc, ws_pull = ws[:a], ws[a:]
+            tile_div = None if flags & MAXK_HYBRID_PRESCALED else row_div
+
+            def tiles(acc, stream):
+                _capi.check(L.maxk_sspmm_backward_pull_tiles(
+                    _ptr(grad_output), _ptr(tile_div), _ptr(cbsr_idx), _ptr(tl), _ptr(te), n_t,
+                    _ptr(bp), _ptr(bt), _ptr(ent), shift, S, acc, _ptr(out), num_rows, num_cols,
+                    ent.shape[0], D, k, _ptr(ws_pull), ws_pull.numel(), stream),
+                    "maxk_sspmm_backward_pull_tiles")
+            main = torch.cuda.current_stream(dev)
+            side = _side_stream(dev)
+            side.wait_stream(main)
+            tiles(MAXK_PULL_NO_REDUCE, ctypes.c_void_p(side.cuda_stream))
+            _capi.check(L.maxk_sspmm_backward_csc(
+                _ptr(oip), _ptr(oix), _ptr(oval), _ptr(grad_output), _ptr(row_div),
+                _ptr(cbsr_idx), _ptr(ocp), _ptr(oeid), _ptr(out), num_rows, num_cols, oix.numel(),
+                D, k, 0, _ptr(ws_csc), ws_csc.numel(), _stream(dev)), "maxk_sspmm_backward_csc")
+            main.wait_stream(side)
+            tiles(MAXK_PULL_REDUCE_ONLY | 1, _stream(dev))
+        # the side stream is joined to the caller's stream before the call returns, so what
+        # it read (ws included) is free for reuse in that stream's order
         return out
     if mode == "pull":
         tptr, ent, shift, S = (plan if plan is not None else
                                pull_plan(indptr, indices, values, num_cols, k, D))
         if row_div is not None and E > 0 and _prescale():
-            nb = int(L.maxk_bucket_count(num_cols, shift))
-            sc = _scaled_entries(ent, torch.arange(S * nb, device=dev), torch.diff(tptr), nb,
-                                 -(-num_rows // S), row_div)
+            sc = _scaled_entries(ent, None, tptr, num_rows, num_cols, shift, S, row_div)
             if sc is not None:
                 ent, row_div = sc, None
         ws_bytes = L.maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, D, k, S)

@@ -61,6 +61,20 @@ SIGNATURES = {
     "maxk_pull_plan_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32]),
     "maxk_pull_plan": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _sz,
                                       _p]),
+    "maxk_backward_mode_auto": (ctypes.c_int, [_i64, _i64, _i64, _i32, _i32, ctypes.c_double]),
+    "maxk_pull_locality": (ctypes.c_int, [_p, _p, _i64, _i64, _i32,
+                                          ctypes.POINTER(ctypes.c_double), _p, _sz, _p]),
+    "maxk_hybrid_plan_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32]),
+    "maxk_hybrid_plan": (ctypes.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _i64, _i32, _i32,
+                                        ctypes.c_float, _p, _p, _p, _p, _p, _p, _p, _p,
+                                        ctypes.POINTER(_i64), _p, _sz, _p]),
+    "maxk_pull_entries_scale": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p,
+                                               _p]),
+    "maxk_sspmm_backward_hybrid_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i64]),
+    "maxk_sspmm_backward_hybrid": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _p, _p, _p, _i64,
+                                                  _i32, _i32, _p, _p, _p, _i64, _p, _p, _i32, _p,
+                                                  _i64, _i64, _i32, _i32, _p, _sz, _p, _p, _p,
+                                                  _p]),
     "maxk_topk_cbsr": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_u8": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_cbsr_scatter_dense": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),

@@ -164,19 +164,20 @@ def test_backward_mode_resolution():
     assert mk._bwd_mode("auto", 64, **proteins) == "pull"
     assert mk._bwd_mode("auto", 32, **products) == "csc"
     assert mk._bwd_mode("auto", 16, **products, dim=256) == "csc"
-    # a sparse graph whose vertex order groups its neighbours (pull_locality >= 1.5): "hybrid";
-    # randomly labelled: csc (the locality is read off the CSR, sizes from the keywords)
-    V, deg = 1 << 20, 8
-    rows = torch.arange(V).repeat_interleave(deg)
-    band = (rows + torch.arange(deg).repeat(V)) % V
-    ip = torch.arange(0, V * deg + 1, deg, dtype=torch.int32)
-    ix_band = torch.sort(band.view(V, deg), 1).values.flatten().to(torch.int32)
-    ix_rand = torch.sort(torch.randint(0, V, (V, deg), generator=torch.Generator().manual_seed(0)),
-                         1).values.flatten().to(torch.int32)
-    assert mk._bwd_mode("auto", 32, **products, dim=256, graph=(ip, ix_band)) == "hybrid"
-    assert mk._bwd_mode("auto", 32, **products, dim=256, graph=(ip, ix_rand)) == "csc"
-    assert mk._bwd_mode("auto", 30, **products, dim=256, graph=(ip, ix_band)) == "csc"
-    assert mk._bwd_mode("auto", 16, **reddit, dim=256, graph=(ip, ix_rand)) == "pull"
+    # a sparse graph whose vertex order groups its neighbours (pull_locality >= 1.5): "hybrid"
+    # (the C ABI's rule on the locality; tests/test_hybrid_gpu.py reads it off real CSRs)
+    from maxk_cuda_kernels import _capi
+    L = _capi.load()
+    P = (products["num_rows"], products["num_cols"], products["num_e"])
+    assert L.maxk_backward_mode_auto(*P, 256, 32, 2.0) == 3    # MAXK_BWD_HYBRID
+    assert L.maxk_backward_mode_auto(*P, 256, 32, 1.5) == 3
+    assert L.maxk_backward_mode_auto(*P, 256, 32, 1.02) == 1   # MAXK_BWD_CSC
+    assert L.maxk_backward_mode_auto(*P, 256, 32, -1.0) == 1   # locality unknown
+    assert L.maxk_backward_mode_auto(*P, 256, 30, 9.0) == 1    # k % 4 != 0
+    assert L.maxk_backward_mode_auto(*P, 9, 32, 9.0) == 1      # dim % 4 != 0
+    R = (reddit["num_rows"], reddit["num_cols"], reddit["num_e"])
+    assert L.maxk_backward_mode_auto(*R, 256, 16, 1.0) == 0    # MAXK_BWD_PULL
+    assert L.maxk_backward_mode_auto(*R, -1, 16, -1.0) == 0    # dim unknown
     # a small gradient (Flickr, 23 MB) stays cache-resident: pull however sparse the graph
     flickr = dict(num_e=989_006, num_cols=89_250, num_rows=89_250)
     assert mk._bwd_mode("auto", 16, **flickr) == "csc"
@@ -234,37 +235,3 @@ def test_pull_slice_rule():
     assert L.maxk_sspmm_backward_pull_workspace_size(232965, 232965, 256, 16, 65) == \
         gp + 65 * 228 * (16 << 10) * 4 + selq
     assert L.maxk_sspmm_backward_pull_workspace_size(10, 10, 0, 16, 1) == 0
-
-
-def test_scaled_pull_entries():
-    """The pull entries pre-divided by their source row's row_div (maxk_cuda_kernels.
-    _scaled_entries): entry {row in slice | column << 16, weight bits} of tile t = s*nb + j
-    belongs to row s*rps + (row in slice); the weight becomes weight / row_div[row], the key
-    word is unchanged, and the copy is cached per (entries, divisor tensor, version)."""
-    import maxk_cuda_kernels as mk
-    g = torch.Generator().manual_seed(3)
-    S, nb, rps, V = 3, 4, 5, 13
-    counts = torch.randint(0, 4, (S * nb,), generator=g)
-    E = int(counts.sum())
-    tiles = torch.arange(S * nb)
-    t_of = torch.repeat_interleave(tiles, counts)
-    rin = torch.randint(0, rps, (E,), generator=g)
-    rin = torch.where(t_of // nb * rps + rin < V, rin, 0)
-    col = torch.randint(0, 1 << 10, (E,), generator=g)
-    w = torch.rand(E, generator=g)
-    ent = torch.stack([rin | (col << 16), w.view(torch.int32).long()], 1).to(torch.int32)
-    div = torch.rand(V, generator=g) + 0.5
-    sc = mk._scaled_entries(ent, tiles, counts, nb, rps, div)
-    assert torch.equal(sc[:, 0], ent[:, 0])
-    rows = t_of // nb * rps + rin
-    assert torch.equal(sc[:, 1].view(torch.float32), w / div[rows])
-    assert mk._scaled_entries(ent, tiles, counts, nb, rps, div) is sc  # cached
-    div.mul_(2.0)
-    sc2 = mk._scaled_entries(ent, tiles, counts, nb, rps, div)  # version moved: rebuilt
-    assert torch.equal(sc2[:, 1].view(torch.float32), w / div[rows])
-    # listed tiles (the hybrid): only some tiles, in increasing order
-    lt = torch.tensor([1, 6, 11])
-    sub = torch.cat([ent[int(counts[:t].sum()):int(counts[:t + 1].sum())] for t in lt.tolist()])
-    sc3 = mk._scaled_entries(sub, lt, counts[lt], nb, rps, div)
-    r3 = torch.repeat_interleave(lt, counts[lt]) // nb * rps + (sub[:, 0].long() & 0xffff)
-    assert torch.equal(sc3[:, 1].view(torch.float32), sub[:, 1].view(torch.float32) / div[r3])

@@ -172,16 +172,19 @@ def test_locality_order_groups_planted_communities():
     assert near(rows2, ix2) > 0.85 > 0.35 > near(rows, ix)
 
 
-def test_pull_locality():
+@pytest.mark.gpu
+def test_pull_locality(cuda):
+    """maxk_pull_locality (C ABI, one kernel pass): a community graph in locality order has
+    far more edges per occupied (row, bucket) than randomly labelled."""
     import maxk_cuda_kernels as mk
     import maxk_graph
     V, E = 4000, 4000 + 2 * 60000
     ip, ix = maxk_graph.community_graph(V, E, 0.75, 30, 8, 0.95, 2, torch.device("cpu"))
-    rnd = mk.pull_locality(ip, ix, 7)
+    rnd = mk.pull_locality(ip.to(cuda), ix.to(cuda), 7)
     ip2, ix2, _ = maxk_graph.permute_graph(ip, ix, maxk_graph.locality_order(ip, ix))
-    ordered = mk.pull_locality(ip2, ix2, 7)
+    ordered = mk.pull_locality(ip2.to(cuda), ix2.to(cuda), 7)
     assert ordered > 2 * rnd
     # one row, columns 0..9 and 200..204 -> buckets of 128: {0}, {1}: 15 edges in 2 pairs
-    one = torch.tensor([0, 15], dtype=torch.int32)
-    cols = torch.tensor(list(range(10)) + list(range(200, 205)), dtype=torch.int32)
+    one = torch.tensor([0, 15], dtype=torch.int32, device=cuda)
+    cols = torch.tensor(list(range(10)) + list(range(200, 205)), dtype=torch.int32, device=cuda)
     assert mk.pull_locality(one, cols, 7) == 7.5
