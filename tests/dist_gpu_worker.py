@@ -4,12 +4,17 @@ collectives staged through host memory (N processes share the device, so each ke
 hardware queue: tools/share_probe.py).  Reads the graph and features the parent wrote, runs
 forward + backward through maxk_dist in both exchange modes and writes its rows back.
 
-    python tests/dist_gpu_worker.py DIR RANK WORLD PORT
+    python tests/dist_gpu_worker.py DIR RANK WORLD PORT [BACKEND]
+
+BACKEND "nccl" (RCCL): one GPU per rank (cuda:RANK), collectives on device over xGMI; only
+where at least WORLD GPUs are visible (tests/test_dist_gpu.py skips it otherwise).
 """
 import os
 import sys
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")  # before HIP starts
+BACKEND = sys.argv[5] if len(sys.argv) > 5 else "gloo"
+if BACKEND == "gloo":
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")  # ranks share one device; before HIP starts
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -25,9 +30,14 @@ def main(d, rank, world, port):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
+    if BACKEND == "nccl":
+        dev = torch.device("cuda", rank)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
     with np.load(os.path.join(d, "graph.npz"), allow_pickle=False) as z:
         g = {n: z[n] for n in z.files}
     k, D = int(g["k"]), int(g["D"])

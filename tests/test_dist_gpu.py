@@ -81,14 +81,15 @@ def close(a, ref, tol):
     assert not bad.any(), f"{bad.sum()} elements off; max err {err.max():.3e}"
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_world_n_on_one_gpu(graph, single, world):
+def _run_world(graph, single, world, backend):
     d, g = graph
     y1, gs1, yo, go = single
     port = _free_port()
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="1")
+    env = dict(os.environ)
+    if backend == "gloo":
+        env["GPU_MAX_HW_QUEUES"] = "1"
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_gpu_worker.py"), str(d),
-                               str(r), str(world), str(port)], env=env)
+                               str(r), str(world), str(port), backend], env=env)
              for r in range(world)]
     try:
         rcs = [p.wait(timeout=100) for p in procs]
@@ -110,3 +111,17 @@ def test_sharded_world_n_on_one_gpu(graph, single, world):
                 close(z[f"{mode}_gs"], go[v0:v1], 1e-4)
                 covered += v1 - v0
         assert covered == V
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_world_n_on_one_gpu(graph, single, world):
+    _run_world(graph, single, world, "gloo")
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_nccl_one_gpu_per_rank(graph, single, world):
+    """The RCCL path the driver's N-GPU bench takes (one rank per GPU, device collectives over
+    xGMI); skipped where fewer than `world` GPUs are visible (the one-GPU box)."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs, {torch.cuda.device_count()} visible")
+    _run_world(graph, single, world, "nccl")
