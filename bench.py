@@ -303,8 +303,9 @@ def main():
     ap.add_argument("--reorder", action="store_true",
                     help="relabel the graph once by maxk_graph.locality_order (communities "
                          "contiguous) before sharding and timing")
-    ap.add_argument("--dist-mode", default="gather", choices=["gather", "halo"],
-                    help="N > 1: all-gather every CBSR row, or exchange only the halo rows")
+    ap.add_argument("--dist-mode", default="auto", choices=["auto", "gather", "halo"],
+                    help="N > 1: all-gather every CBSR row, or exchange only the halo rows "
+                         "(auto: halo when every shard's halo is at most 60 %% of the vertices)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -567,7 +568,7 @@ def main():
     if world > 1:
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
                       "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
-                      "dist_mode": args.dist_mode, "rows_per_rank_max": vmax,
+                      "dist_mode": shard.mode, "rows_per_rank_max": vmax,
                       "edges_this_rank0": El, "cols_this_rank0": n_cols,
                       "exchange_bytes_rank0": shard.exchange_bytes(k)})
 

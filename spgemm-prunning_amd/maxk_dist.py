@@ -7,7 +7,8 @@ those vertices.  There is no reference counterpart (the reference is
 single-GPU); the oracle for this path is "identical to the
 1-GPU result".
 
-Two exchange modes, the same result:
+Two exchange modes, the same result ("auto" picks halo when every shard's halo is at most
+HALO_SHARE of the vertices, else gather):
   "gather" (default)  forward: one all-gather of every vertex's CBSR row (k f32 +
             k u8); backward: the local push into a CBSR-shaped gradient for ALL
             vertices, then a reduce-scatter that sums the partials on the owners.
@@ -73,6 +74,15 @@ def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, gro
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
+def _all_reduce_max(t: torch.Tensor, group=None) -> None:
+    if _staged(group) and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+
+
 def balanced_bounds(row_ptr: torch.Tensor, world: int) -> List[int]:
     """Row boundaries [0 = b0 <= b1 <= ... <= b_world = V] with ~E/world edges per shard."""
     rp = row_ptr.detach().to("cpu", torch.int64)
@@ -111,14 +121,20 @@ class ShardedMaxK:
     mode "halo":   column space = this shard's halo (the distinct columns of its edges, in
                    global-id order).  n_cols is its size either way."""
 
-    MODES = ("gather", "halo")
+    MODES = ("gather", "halo", "auto")
+    # mode "auto": halo when every shard's halo is at most this share of the vertices (an
+    # ordered graph's shards need a fraction of the others' rows: the exchange shrinks and
+    # the per-column work -- record pack, selector ordering, tile reduce, phase-2 walk --
+    # covers the halo only); gather otherwise (a randomly labelled graph's halo is nearly
+    # every vertex, and one all-gather / reduce-scatter beats all-to-allv of the same bytes)
+    HALO_SHARE = 0.6
 
     def __init__(self, row_ptr: torch.Tensor, col_idx: torch.Tensor, values: torch.Tensor,
                  rank: int, world: int, group=None, device=None, kernels=None,
                  bounds: Optional[List[int]] = None, mode: str = "gather"):
         if mode not in self.MODES:
             raise ValueError(f"mode must be one of {self.MODES}, got {mode!r}")
-        self.rank, self.world, self.group, self.mode = rank, world, group, mode
+        self.rank, self.world, self.group = rank, world, group
         self.device = torch.device(device) if device is not None else row_ptr.device
         self.kernels = kernels if kernels is not None else _HipKernels()
         self.bounds = bounds if bounds is not None else balanced_bounds(row_ptr, world)
@@ -132,6 +148,13 @@ class ShardedMaxK:
         self.row_ptr = (rp[self.v0:self.v1 + 1] - e0).to(torch.int32).contiguous()
         cols = col_idx[e0:e1].to(self.device, torch.int64)
         starts = torch.tensor(b, dtype=torch.int64, device=self.device)
+        if mode == "auto":  # every rank must pick the same collectives: decide on the max
+            share = torch.tensor([torch.unique(cols).numel() / max(1, self.V)],
+                                 dtype=torch.float64, device=self.device)
+            _all_reduce_max(share, group)
+            self.halo_share = float(share.item())
+            mode = "halo" if self.halo_share <= self.HALO_SHARE else "gather"
+        self.mode = mode
         if mode == "gather":
             owner = torch.searchsorted(starts[1:], cols, right=True)
             self.col_idx = (owner * self.vmax + (cols - starts[owner])).to(torch.int32).contiguous()

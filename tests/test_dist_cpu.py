@@ -122,7 +122,7 @@ def _single(V, D, k, seed, use_div):
     return y, gs
 
 
-@pytest.mark.parametrize("mode", ["gather", "halo"])
+@pytest.mark.parametrize("mode", ["gather", "halo", "auto"])
 @pytest.mark.parametrize("world,use_div,bounds", [(2, True, None), (3, False, None),
                                                   (4, True, None),
                                                   (3, True, [0, 150, 150, 400])])
@@ -206,9 +206,11 @@ def _local_worker(rank, world, port, args, D, k, q):
         tv, ti = oracle.topk(rng.standard_normal((V, D)).astype(np.float32), k)
         g = rng.standard_normal((V, D)).astype(np.float32)
         res = {}
-        for mode in ("gather", "halo"):
+        for mode in ("gather", "halo", "auto"):
             shard = maxk_dist.ShardedMaxK(rp, col, val, rank, world, kernels=OracleKernels(),
                                           mode=mode)
+            if mode == "auto":  # a local graph's shards need few rows: the halo exchange
+                assert shard.mode == "halo" and shard.halo_share <= shard.HALO_SHARE
             v0, v1 = shard.v0, shard.v1
             val_l = torch.from_numpy(tv[v0:v1]).requires_grad_(True)
             y = maxk_dist.sharded_maxk_spgemm(shard, val_l, torch.from_numpy(ti[v0:v1]), D)
