@@ -18,6 +18,20 @@ void set_error(const char *fmt, ...) {
 
 void clear_error() { g_err[0] = '\0'; }
 
+__global__ void zero_words_kernel(uint32_t *__restrict__ p, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = 0u;
+}
+
+int zero_words(void *p, int64_t n, hipStream_t s) {
+    if (n <= 0) return MAXK_OK;
+    const int64_t blocks = ceil_div(n, kBlock);
+    hipLaunchKernelGGL(zero_words_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)),
+                       dim3(kBlock), 0, s, reinterpret_cast<uint32_t *>(p), n);
+    MAXK_LAUNCHED("zero_words_kernel");
+    return MAXK_OK;
+}
+
 }  // namespace maxk
 
 extern "C" int maxk_version(void) { return 100; }

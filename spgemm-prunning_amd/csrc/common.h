@@ -208,6 +208,13 @@ inline int lanes_per_edge(int k) {
 // ---- device helpers ----
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Zero n 4-byte words on the stream with a kernel.  Launch paths use this instead of
+// hipMemsetAsync: a memset captured into a hipGraph (ROCm 7.2) zeroed its buffer on the first
+// replay only, so the hybrid backward (tests/test_parity_gpu.py hipgraph capture) summed onto
+// stale values from the second replay on (tools/capture_probe*.py).
+__global__ void zero_words_kernel(uint32_t *__restrict__ p, int64_t n);
+int zero_words(void *p, int64_t n, hipStream_t s);
+
 // The hardware hands workgroup b to XCD b % 8 (each XCD has its own L2).  With
 // grid = 8 * per, logical block (b % 8) * per + b / 8 makes XCD x run the contiguous
 // logical range [x * per, (x + 1) * per) in launch order, so work items that are

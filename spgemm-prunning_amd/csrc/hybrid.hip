@@ -440,7 +440,7 @@ extern "C" int maxk_sspmm_backward_hybrid(
                                              ws_csc, a, stream))
             return rc;
     } else {
-        MAXK_HIP(hipMemsetAsync(grad_cbsr, 0, (size_t)num_cols * dim_k * 4, s));
+        if (int rc = zero_words(grad_cbsr, num_cols * dim_k, s)) return rc;
     }
     if (overlap) {
         MAXK_HIP(hipStreamWaitEvent(s, reinterpret_cast<hipEvent_t>(ev_join), 0));

@@ -1363,7 +1363,7 @@ extern "C" int maxk_sspmm_backward(const int32_t *row_ptr, const int32_t *col_id
     hipStream_t s = as_stream(stream);
     if (num_cols > 0) {
         MAXK_REQUIRE(grad_cbsr != nullptr, "grad_cbsr must not be NULL");
-        MAXK_HIP(hipMemsetAsync(grad_cbsr, 0, (size_t)num_cols * dim_k * sizeof(float), s));
+        if (int rc = zero_words(grad_cbsr, num_cols * dim_k, s)) return rc;
     }
     if (num_rows == 0 || num_e == 0) return MAXK_OK;
     MAXK_REQUIRE(row_ptr && col_idx && edge_val && grad_out && cbsr_idx,

@@ -229,8 +229,15 @@ def test_c_abi_hybrid_backward(cuda, side):
     cv, ci = O.topk(rng.standard_normal((V, D), dtype=np.float32), k)
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = torch.clamp(torch.diff(ip).float(), min=1.0)
-    tl, te, bp, bt, ent, shift, S, (oip, oix, oval, (ocp, oeid)) = mk.hybrid_plan(
-        ip, ix, val, V, k, D, density=0.3, cache=False)
+    # a density between the sparsest tile's and the others': some tiles pulled, some not
+    tptr, _, _, S0 = mk.pull_plan(ip, ix, val, V, k, D, cache=False)
+    cnt = torch.diff(tptr.long()).double()
+    rows_in = -(-V // S0)
+    dens = torch.unique(cnt[cnt > 0] / rows_in).sort().values
+    assert dens.numel() >= 2
+    plan = mk.hybrid_plan(ip, ix, val, V, k, D, density=float(dens[0] + dens[1]) / 2,
+                          cache=False)
+    tl, te, bp, bt, ent, shift, S, (oip, oix, oval, (ocp, oeid)) = plan
     assert tl.numel() > 0 and oix.numel() > 0
     gt, ct = torch.from_numpy(g).to(cuda), torch.from_numpy(ci).to(cuda)
     out = torch.empty(V, k, device=cuda)

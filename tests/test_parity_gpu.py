@@ -663,7 +663,7 @@ def test_hipgraph_capture(mk, cuda):
     close(out, z["y_ref"])
 
 
-@pytest.mark.parametrize("mode", ["pull", "bucket", "csc", "hybrid"])
+@pytest.mark.parametrize("mode", ["pull", "bucket", "csc", "hybrid", "atomic"])
 def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch, mode):
     """Default (validate-once) mode: the first call may be inside a capture; forward and the
     two-phase backward (with its plan built beforehand) both replay correctly."""
