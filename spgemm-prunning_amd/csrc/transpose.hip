@@ -281,10 +281,17 @@ static int pull_parts_of(int32_t dim_k) {
 // 40-66, k = 32 (2 parts) at 33.  Past 3 parts the gain stops: k = 64 (4 parts) runs 5.32 ms
 // at S = 20-22 against 5.74 at 17 (profiles/r02/tune/pull_slices_k64.txt), so the factor is
 // capped at 3 (proteins k = 64 is flat over S = 8-12).
+// r03 (profiles/r03/tune/pull_slices.txt, two repeats each): the narrower a part's share of
+// a row's columns, the more rows a slice may hold -- k = 8 (one 8-slot part) best at
+// S = 44 (5.3 MiB; 1.400 ms against 1.418 at S = 66), k = 16 (two 8-slot parts) at S = 28
+// (4.1 MiB per part; 2.120 against 2.145 at S = 33), k = 32 (two 16-slot parts) still at 33.
 extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
     const int parts = dim_k % 4 == 0 ? pull_parts_of(dim_k) : 1;
-    const int64_t per = maxk::kPullSliceBytes * (parts < 3 ? parts : 3);
+    const int64_t part_bytes = dim_k <= 8    ? maxk::kPullSliceBytes * 3 / 2
+                               : dim_k <= 16 ? maxk::kPullSliceBytes * 33 / 28
+                                             : maxk::kPullSliceBytes;
+    const int64_t per = part_bytes * (parts < 3 ? parts : 3);
     int64_t s = (num_rows * dim_origin * 4 + per - 1) / per;
     const int64_t lo = (num_rows + 65535) / 65536;  // rows within a slice fit 16 bits
     s = s < lo ? lo : s;

@@ -221,11 +221,11 @@ def test_pull_slice_rule():
     buckets, k] per slice."""
     from maxk_cuda_kernels import _capi
     L = _capi.load()
-    assert L.maxk_pull_slices(232965, 256, 16) == 33  # Reddit: 238.6 MB of G rows, 2 parts
-    assert L.maxk_pull_slices(232965, 256, 8) == 66   # 1 part
+    assert L.maxk_pull_slices(232965, 256, 16) == 28  # Reddit: 238.6 MB of G rows, 2 parts
+    assert L.maxk_pull_slices(232965, 256, 8) == 44   # 1 part
     assert L.maxk_pull_slices(232965, 256, 32) == 33  # 2 parts
     assert L.maxk_pull_slices(232965, 256, 64) == 22  # 4 parts, factor capped at 3
-    assert L.maxk_pull_slices(29121, 256, 16) == 5    # one of 8 row shards
+    assert L.maxk_pull_slices(29121, 256, 16) == 4    # one of 8 row shards
     assert L.maxk_pull_slices(1, 256, 16) == 1 and L.maxk_pull_slices(0, 256, 16) == 1
     assert L.maxk_pull_slices(100_000_000, 256, 16) == 256
     assert L.maxk_pull_slices(2_449_029, 256, 64) == 228
