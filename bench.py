@@ -458,25 +458,43 @@ def main():
     torch.cuda.synchronize()
     t_plan = time.perf_counter() - t_plan
 
-    # HIP events on the stream the kernels run on (torch's current stream)
+    pipelined = world > 1 and shard.pipeline > 1
+    if pipelined:  # the parts' plans (per-graph setup, untimed), in the bench's backward mode
+        shard.kernels.bwd_mode = args.bwd_mode
+        t_plan = time.perf_counter()
+        for j in range(shard.pipeline):
+            shard.plan(k, D, j)
+        torch.cuda.synchronize()
+        t_plan = time.perf_counter() - t_plan
+
+    # HIP events on the stream the kernels run on (torch's current stream).  N > 1: the
+    # forward interval holds the CBSR exchange and the backward one the gradient exchange
+    # (pipelined with the kernels part by part, maxk_dist.ShardedMaxK.aggregate / grad)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    saved = None
 
     def step(ev=None):
-        nonlocal cv_all, ci_all
-        if world > 1:
-            cv_all, ci_all = shard.gather_cbsr(cv_loc[:nl], ci_loc[:nl])
+        nonlocal cv_all, ci_all, saved
         if ev:
             ev[0].record()
-        mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y, chunk=args.chunk,
-                          validate=False)
+        if pipelined:
+            _, saved = shard.aggregate(cv_loc[:nl], ci_loc[:nl], D, out=y)
+        else:
+            if world > 1:
+                cv_all, ci_all = shard.gather_cbsr(cv_loc[:nl], ci_loc[:nl])
+            mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y,
+                              chunk=args.chunk, validate=False)
         if ev:
             ev[1].record()
-        mk.sspmm_backward(l_row_ptr, l_col, l_val, l_G, ci_all, out=gs_all, chunk=args.chunk,
-                          validate=False, mode=args.bwd_mode, plan=plan)
+        if pipelined:
+            gs_loc[:nl] = shard.grad(l_G, saved)
+        else:
+            mk.sspmm_backward(l_row_ptr, l_col, l_val, l_G, ci_all, out=gs_all,
+                              chunk=args.chunk, validate=False, mode=args.bwd_mode, plan=plan)
+            if world > 1:
+                gs_loc[:nl] = shard.scatter_grad(gs_all)
         if ev:
             ev[2].record()
-        if world > 1:
-            gs_loc[:nl] = shard.scatter_grad(gs_all)
 
     stage(f"backward plan ({args.bwd_mode}) {t_plan:.3f}s")
     for _ in range(args.warmup):
@@ -500,9 +518,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # ---- sanity: forward/backward adjoint identity on the timed buffers
+    # ---- sanity: forward/backward adjoint identity on the timed buffers (summed over ranks:
+    # each rank's output rows against its G rows, its CBSR rows against their gradient)
     a = (y.double() * l_G.double()).sum()
-    b = (cv_all.double() * gs_all.double()).sum()
+    gs_own = gs_all[:nl] if world == 1 else gs_loc[:nl]
+    b = (cv_loc[:nl].double() * gs_own.double()).sum()
     if dist:
         ab = torch.stack([a, b])
         if backend != "nccl":
@@ -568,7 +588,8 @@ def main():
     if world > 1:
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
                       "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
-                      "dist_mode": shard.mode, "rows_per_rank_max": vmax,
+                      "dist_mode": shard.mode, "dist_pipeline": shard.pipeline,
+                      "rows_per_rank_max": vmax,
                       "edges_this_rank0": El, "cols_this_rank0": n_cols,
                       "exchange_bytes_rank0": shard.exchange_bytes(k)})
 

@@ -74,6 +74,15 @@ int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_idx, const fl
                         float *out, int64_t num_rows, int64_t num_cols, int64_t num_e,
                         int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
                         void *workspace, size_t workspace_bytes, void *stream);
+/* The same product added onto out (out += ...; out must hold valid values): a row range's
+ * result summed over several column ranges of A, e.g. the sharded forward's pipelined halves
+ * (maxk_dist.py), without a separate pass over out.  Same arguments and workspace. */
+int maxk_spgemm_forward_accumulate(const int32_t *row_ptr, const int32_t *col_idx,
+                                   const float *edge_val, const float *cbsr_val,
+                                   const uint8_t *cbsr_idx, const float *row_div, float *out,
+                                   int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                   int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                                   void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Backward outer-product sampled SpMM (SSpMM):

@@ -317,9 +317,10 @@ struct EdgeWalker {
 };
 
 // dst[0:D] = (sum_g acc[g][0:D]) / div ; acc = 0.  One wave; copies of stride DS.
+// add (maxk_spgemm_forward_accumulate): dst[0:D] += instead.
 template <int NC>
 __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict__ dst, int D,
-                                          float div, bool scale, int lane) {
+                                          float div, bool scale, int lane, bool add = false) {
     wave_lds_fence();
     if ((D & 3) == 0) {
         for (int j = lane * 4; j < D; j += kWave * 4) {
@@ -341,6 +342,13 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
                 a.z = a.z / div;
                 a.w = a.w / div;
             }
+            if (add) {
+                const float4 o = *reinterpret_cast<const float4 *>(&dst[j]);
+                a.x += o.x;
+                a.y += o.y;
+                a.z += o.z;
+                a.w += o.w;
+            }
             *reinterpret_cast<float4 *>(&dst[j]) = a;
         }
     } else {
@@ -351,7 +359,7 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
                 a += acc[g * DS + j];
                 acc[g * DS + j] = 0.f;
             }
-            dst[j] = scale ? a / div : a;
+            dst[j] = (scale ? a / div : a) + (add ? dst[j] : 0.f);
         }
     }
     wave_lds_fence();
@@ -363,7 +371,7 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     const float *__restrict__ edge_val, const uint8_t *__restrict__ rec, int RS,
     const float *__restrict__ row_div, float *__restrict__ out, float *__restrict__ slab,
     int32_t *__restrict__ slab_row, int num_rows, int64_t num_e, int D, int DS, int k,
-    int chunk, int n_items) {
+    int chunk, int n_items, int accumulate) {
     constexpr int NC = kWave / KG;  // LDS copies per wave (one per edge group)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wid = threadIdx.x / kWave;
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
                 for (int j = 0; j < m; ++j) {
                     const float div = row_div ? row_div[r + j] : 1.f;
                     flush_row<1>(acc + j * DS, DS, out + (int64_t)(r + j) * D, D, div,
-                                 row_div != nullptr, lane);
+                                 row_div != nullptr, lane, accumulate != 0);
                 }
                 r += m;
                 continue;
@@ -455,7 +463,8 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
             EdgeWalker<KG, U, WIDE>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se, k, DS - 1,
                                    lane);
         const float div = row_div ? row_div[r] : 1.f;
-        flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane);
+        flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane,
+                      accumulate != 0);
         ++r;
     }
 }
@@ -499,7 +508,8 @@ FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, i
 template <int KG>
 void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 const float *edge_val, const uint8_t *rec, const float *row_div, float *out,
-                float *slab, int32_t *slab_row, int num_rows, int64_t num_e, int D, int k) {
+                float *slab, int32_t *slab_row, int num_rows, int64_t num_e, int D, int k,
+                int accumulate) {
     constexpr int U = MAXK_FWD_U;
     constexpr int NC = kWave / KG;
     const size_t lds = (size_t)kWavesPerBlock * NC * L.DS * sizeof(float);
@@ -510,11 +520,11 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
     if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32))
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false>), grid, dim3(kBlock), lds, s, row_ptr,
                            col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows,
-                           num_e, D, L.DS, k, L.chunk, L.n_items);
+                           num_e, D, L.DS, k, L.chunk, L.n_items, accumulate);
     else
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, true>), grid, dim3(kBlock), lds, s, row_ptr,
                            col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows,
-                           num_e, D, L.DS, k, L.chunk, L.n_items);
+                           num_e, D, L.DS, k, L.chunk, L.n_items, accumulate);
 }
 
 }  // namespace
@@ -529,13 +539,12 @@ extern "C" size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t n
     return fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges).total;
 }
 
-extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_idx,
-                                   const float *edge_val, const float *cbsr_val,
-                                   const uint8_t *cbsr_idx, const float *row_div, float *out,
-                                   int64_t num_rows, int64_t num_cols, int64_t num_e,
-                                   int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
-                                   void *workspace, size_t workspace_bytes, void *stream) {
-    clear_error();
+namespace {
+int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                 const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div, float *out,
+                 int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                 int32_t dim_k, int32_t chunk_edges, void *workspace, size_t workspace_bytes,
+                 void *stream, int accumulate) {
     MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range: %lld",
                  (long long)num_rows);
     MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
@@ -585,7 +594,7 @@ extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_id
 #define MAXK_CASE(KGV)                                                                     \
     case KGV:                                                                              \
         launch_fwd<KGV>(L, s, row_ptr, col_idx, edge_val, rec, row_div, out, slab,         \
-                        slab_row, nr, num_e, D, k);                                        \
+                        slab_row, nr, num_e, D, k, accumulate);                            \
         break;
         MAXK_CASE(8)
         MAXK_CASE(16)
@@ -598,4 +607,31 @@ extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_id
     }
     MAXK_LAUNCHED("spgemm_fwd_kernel");
     return launch_slab_fixup<0>(slab, slab_row, out, D, L.n_items, s);
+}
+}  // namespace
+
+extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_idx,
+                                   const float *edge_val, const float *cbsr_val,
+                                   const uint8_t *cbsr_idx, const float *row_div, float *out,
+                                   int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                   int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                                   void *workspace, size_t workspace_bytes, void *stream) {
+    clear_error();
+    return forward_impl(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out, num_rows,
+                        num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
+                        workspace_bytes, stream, 0);
+}
+
+extern "C" int maxk_spgemm_forward_accumulate(const int32_t *row_ptr, const int32_t *col_idx,
+                                              const float *edge_val, const float *cbsr_val,
+                                              const uint8_t *cbsr_idx, const float *row_div,
+                                              float *out, int64_t num_rows, int64_t num_cols,
+                                              int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                                              int32_t chunk_edges, void *workspace,
+                                              size_t workspace_bytes, void *stream) {
+    clear_error();
+    if (num_e == 0) return MAXK_OK;  // adds zeros
+    return forward_impl(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out, num_rows,
+                        num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
+                        workspace_bytes, stream, 1);
 }

@@ -198,9 +198,10 @@ def load_warp4_metadata_csc(graph_name: str, num_warps: int = 12,
 def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
                    cbsr_val: torch.Tensor, cbsr_idx: torch.Tensor, dim_origin: int,
                    row_div: Optional[torch.Tensor] = None, chunk: int = 0,
-                   out: Optional[torch.Tensor] = None, validate: Optional[bool] = None
-                   ) -> torch.Tensor:
-    """out[num_rows, D] = diag(1/row_div) . A . scatter(cbsr)  (CSR A: indptr/indices/values)."""
+                   out: Optional[torch.Tensor] = None, validate: Optional[bool] = None,
+                   accumulate: bool = False) -> torch.Tensor:
+    """out[num_rows, D] = diag(1/row_div) . A . scatter(cbsr)  (CSR A: indptr/indices/values).
+    accumulate: out += the product instead (out= required; maxk_spgemm_forward_accumulate)."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32), (cbsr_val, "input_data", torch.float32),
                      (cbsr_idx, "sparse_selector", torch.uint8)):
@@ -219,6 +220,8 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     _validate_call(validate, indptr, indices, num_cols, cbsr_idx, D)
     dev = cbsr_val.device
     if out is None:
+        if accumulate:
+            raise RuntimeError("accumulate=True needs out=")
         out = torch.empty(num_rows, D, dtype=torch.float32, device=dev)
     else:
         _need(out, "out", torch.float32)
@@ -228,11 +231,12 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     E = indices.numel()
     ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, num_cols, E, D, k, chunk)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    fn = L.maxk_spgemm_forward_accumulate if accumulate else L.maxk_spgemm_forward
     with torch.cuda.device(dev):
-        _capi.check(L.maxk_spgemm_forward(
+        _capi.check(fn(
             _ptr(indptr), _ptr(indices), _ptr(values), _ptr(cbsr_val), _ptr(cbsr_idx),
             _ptr(row_div), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws), ws.numel(),
-            _stream(dev)), "maxk_spgemm_forward")
+            _stream(dev)), "maxk_spgemm_forward_accumulate" if accumulate else "maxk_spgemm_forward")
     return out
 
 

@@ -33,6 +33,8 @@ SIGNATURES = {
     "maxk_spgemm_forward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_spgemm_forward": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),
+    "maxk_spgemm_forward_accumulate": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
+                                           _i32, _i32, _i32, _p, _sz, _p]),
     "maxk_sspmm_backward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),

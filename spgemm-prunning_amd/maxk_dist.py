@@ -44,24 +44,32 @@ def _staged(group) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
-def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
-    """out[p * n:(p + 1) * n] = inp of rank p (equal n on every rank)."""
+def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=False):
+    """out[p * n:(p + 1) * n] = inp of rank p (equal n on every rank).  async_op (RCCL): the
+    call is queued on the communicator's stream and its work handle returned; wait() on it
+    makes the current stream wait (the host does not block).  Staged (gloo) calls complete
+    before returning (None)."""
     if _staged(group) and inp.is_cuda:
         tmp = torch.empty(out.shape, dtype=out.dtype)
         dist.all_gather_into_tensor(tmp, inp.cpu(), group=group)
         out.copy_(tmp)
-    else:
-        dist.all_gather_into_tensor(out, inp, group=group)
+        return None
+    return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
-def reduce_scatter_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
-    """out = sum over ranks of inp[rank * n:(rank + 1) * n]."""
+def reduce_scatter_rows(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=False):
+    """out = sum over ranks of inp[rank * n:(rank + 1) * n]; async_op as all_gather_rows."""
     if _staged(group) and inp.is_cuda:
         tmp = torch.empty(out.shape, dtype=out.dtype)
         dist.reduce_scatter_tensor(tmp, inp.cpu(), group=group)
         out.copy_(tmp)
-    else:
-        dist.reduce_scatter_tensor(out, inp, group=group)
+        return None
+    return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
+
+
+def _wait(work) -> None:
+    if work is not None:
+        work.wait()
 
 
 def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None):
@@ -97,21 +105,23 @@ def balanced_bounds(row_ptr: torch.Tensor, world: int) -> List[int]:
 
 
 class _HipKernels:
-    def __init__(self):
+    def __init__(self, bwd_mode=None):
         import maxk_cuda_kernels as mk
         self.mk = mk
+        self.bwd_mode = bwd_mode  # None: "auto" per shard (or pipeline part)
 
-    def spgemm_forward(self, indptr, indices, values, cbsr_val, cbsr_idx, D, row_div=None):
+    def spgemm_forward(self, indptr, indices, values, cbsr_val, cbsr_idx, D, row_div=None,
+                       out=None, accumulate=False):
         return self.mk.spgemm_forward(indptr, indices, values, cbsr_val, cbsr_idx, D,
-                                      row_div=row_div)
+                                      row_div=row_div, out=out, accumulate=accumulate)
 
     def sspmm_backward(self, indptr, indices, values, grad, cbsr_idx, row_div=None, plan=None):
         return self.mk.sspmm_backward(indptr, indices, values, grad, cbsr_idx, row_div=row_div,
-                                      plan=plan)
+                                      plan=plan, mode=self.bwd_mode)
 
     def backward_plan(self, indptr, indices, values, num_cols, k, num_rows=None, dim=None):
-        return self.mk.backward_plan(indices, num_cols, k, num_rows=num_rows, indptr=indptr,
-                                     values=values, dim=dim)
+        return self.mk.backward_plan(indices, num_cols, k, mode=self.bwd_mode, num_rows=num_rows,
+                                     indptr=indptr, values=values, dim=dim)
 
 
 class ShardedMaxK:
@@ -122,6 +132,11 @@ class ShardedMaxK:
                    global-id order).  n_cols is its size either way."""
 
     MODES = ("gather", "halo", "auto")
+    # "gather" mode, world > 1: the exchange runs in PIPELINE column parts (each owner's rows
+    # cut into PIPELINE equal ranges, one sub-CSR per range): the forward adds part j's
+    # product while part j+1's all-gather is in flight, and the backward's reduce-scatter of
+    # part j runs beside part j+1's backward (DESIGN.md 7)
+    PIPELINE = 2
     # mode "auto": halo when every shard's halo is at most this share of the vertices (an
     # ordered graph's shards need a fraction of the others' rows: the exchange shrinks and
     # the per-column work -- record pack, selector ordering, tile reduce, phase-2 walk --
@@ -131,7 +146,8 @@ class ShardedMaxK:
 
     def __init__(self, row_ptr: torch.Tensor, col_idx: torch.Tensor, values: torch.Tensor,
                  rank: int, world: int, group=None, device=None, kernels=None,
-                 bounds: Optional[List[int]] = None, mode: str = "gather"):
+                 bounds: Optional[List[int]] = None, mode: str = "gather",
+                 pipeline: Optional[int] = None):
         if mode not in self.MODES:
             raise ValueError(f"mode must be one of {self.MODES}, got {mode!r}")
         self.rank, self.world, self.group = rank, world, group
@@ -157,12 +173,39 @@ class ShardedMaxK:
         self.mode = mode
         if mode == "gather":
             owner = torch.searchsorted(starts[1:], cols, right=True)
-            self.col_idx = (owner * self.vmax + (cols - starts[owner])).to(torch.int32).contiguous()
+            loc = cols - starts[owner]
+            self.col_idx = (owner * self.vmax + loc).to(torch.int32).contiguous()
             self.n_cols = world * self.vmax
         else:
             self._halo_plan(cols, starts)
         self.values = values[e0:e1].to(self.device, torch.float32).contiguous()
         self._plans = {}
+        P = self.PIPELINE if pipeline is None else int(pipeline)
+        self.pipeline = max(1, min(P, self.vmax)) if mode == "gather" and world > 1 else 1
+        if self.pipeline > 1:
+            self._split_parts(owner, loc)
+
+    # ---- pipelined gather mode: column parts (once per graph)
+    def _split_parts(self, owner: torch.Tensor, loc: torch.Tensor) -> None:
+        """Part j = the columns whose row inside their owner lies in [j * vh, (j + 1) * vh);
+        its sub-CSR keeps the shard's rows (CSR order inside each row) and numbers its columns
+        owner * vh + (loc - j * vh), the padded space of that part's all-gather."""
+        P = self.pipeline
+        vh = -(-self.vmax // P)
+        self.vh = vh
+        part = loc // vh
+        counts = torch.diff(self.row_ptr.to(torch.int64))
+        rows_e = torch.repeat_interleave(torch.arange(self.n_local, device=self.device), counts)
+        self.parts = []
+        for j in range(P):
+            m = part == j
+            cnt = torch.bincount(rows_e[m], minlength=self.n_local)
+            rp = torch.zeros(self.n_local + 1, dtype=torch.int64, device=self.device)
+            rp[1:] = torch.cumsum(cnt, 0)
+            col = (owner[m] * vh + (loc[m] - j * vh)).to(torch.int32).contiguous()
+            self.parts.append((rp.to(torch.int32).contiguous(), col,
+                               self.values[m].contiguous()))
+        self.n_cols_part = self.world * vh
 
     # ---- halo send plan (once per graph)
     def _halo_plan(self, cols: torch.Tensor, starts: torch.Tensor) -> None:
@@ -184,9 +227,10 @@ class ShardedMaxK:
         """Bytes this rank sends / receives per step (forward CBSR + backward gradient)."""
         row_f, row_b = k * 5, k * 4  # k f32 + k u8 forward, k f32 backward
         if self.mode == "gather":
-            others = self.n_cols - self.vmax
-            return {"fwd_recv": others * row_f, "fwd_send": (self.world - 1) * self.vmax * row_f,
-                    "bwd_send": others * row_b, "bwd_recv": (self.world - 1) * self.vmax * row_b}
+            rows = self.vh * self.pipeline if self.pipeline > 1 else self.vmax  # padded chunk
+            others = (self.world - 1) * rows
+            return {"fwd_recv": others * row_f, "fwd_send": others * row_f,
+                    "bwd_send": others * row_b, "bwd_recv": others * row_b}
         own = self.recv_counts[self.rank]
         recv_rows = self.n_cols - own
         send_rows = sum(self.send_counts) - self.send_counts[self.rank]
@@ -241,15 +285,87 @@ class ShardedMaxK:
             o += n
         return out
 
-    def plan(self, k: int, D: Optional[int] = None):
+    def plan(self, k: int, D: Optional[int] = None, part: Optional[int] = None):
         """The backward's per-graph plan at width k and feature width D (built once per
-        (k, D); None for a kernel backend without plans, e.g. the CPU oracle in the tests)."""
-        if (k, D) not in self._plans:
+        (k, D) and pipeline part; None for a kernel backend without plans, e.g. the CPU oracle
+        in the tests, or a part without edges)."""
+        key = (k, D, part)
+        if key not in self._plans:
             bp = getattr(self.kernels, "backward_plan", None)
-            self._plans[(k, D)] = (bp(self.row_ptr, self.col_idx, self.values, self.n_cols, k,
-                                      num_rows=self.n_local, dim=D)
-                                   if bp is not None else None)
-        return self._plans[(k, D)]
+            rp, col, val, nc = ((self.row_ptr, self.col_idx, self.values, self.n_cols)
+                                if part is None else self.parts[part] + (self.n_cols_part,))
+            self._plans[key] = (bp(rp, col, val, nc, k, num_rows=self.n_local, dim=D)
+                                if bp is not None and col.numel() > 0 else None)
+        return self._plans[key]
+
+    # ---- one aggregation step (gather + forward; backward + scatter), pipelined or not
+    def aggregate(self, val_local: torch.Tensor, idx_local: torch.Tensor, D: int,
+                  row_div_local=None, out: Optional[torch.Tensor] = None):
+        """(Y_local [n_local, D], saved) -- saved is what grad() needs: the gathered
+        selectors (one tensor, or one per pipeline part)."""
+        if self.pipeline == 1:
+            val_all, idx_all = self.gather_cbsr(val_local, idx_local)
+            y = self.kernels.spgemm_forward(self.row_ptr, self.col_idx, self.values, val_all,
+                                            idx_all, D, row_div=row_div_local,
+                                            **({} if out is None else {"out": out}))
+            return y, idx_all
+        k = val_local.shape[1]
+        dev = val_local.device
+        P, vh = self.pipeline, self.vh
+        sv = torch.zeros(P * vh, k, dtype=val_local.dtype, device=dev)
+        si = torch.zeros(P * vh, k, dtype=idx_local.dtype, device=dev)
+        sv[:self.n_local] = val_local
+        si[:self.n_local] = idx_local
+        # every part's two all-gathers (values, selectors: each lands as the contiguous
+        # [world * vh, k] array the kernels take, no unpacking copy) queued at once, in part order
+        recvs, works = [], []
+        for j in range(P):
+            rv = torch.empty(self.world * vh, k, dtype=sv.dtype, device=dev)
+            ri = torch.empty(self.world * vh, k, dtype=si.dtype, device=dev)
+            wv = all_gather_rows(rv.view(-1), sv[j * vh:(j + 1) * vh].reshape(-1), self.group,
+                                 async_op=True)
+            wi = all_gather_rows(ri.view(-1), si[j * vh:(j + 1) * vh].reshape(-1), self.group,
+                                 async_op=True)
+            recvs.append((rv, ri))
+            works.append((wv, wi))
+        y, saved = out, []
+        for j in range(P):
+            _wait(works[j][0])
+            _wait(works[j][1])
+            val_j, idx_j = recvs[j]
+            saved.append(idx_j)
+            rp, col, val = self.parts[j]
+            if j == 0:  # writes every row (zeros where part 0 has no edges)
+                y = self.kernels.spgemm_forward(rp, col, val, val_j, idx_j, D,
+                                                row_div=row_div_local,
+                                                **({} if y is None else {"out": y}))
+            elif col.numel() > 0:
+                self.kernels.spgemm_forward(rp, col, val, val_j, idx_j, D, row_div=row_div_local,
+                                            out=y, accumulate=True)
+        return y, saved
+
+    def grad(self, grad_local: torch.Tensor, saved, row_div_local=None) -> torch.Tensor:
+        """CBSR gradient of the owned vertices [n_local, k] from aggregate()'s saved state."""
+        if self.pipeline == 1:
+            return self.backward(grad_local, saved, row_div_local)
+        g = grad_local.contiguous()
+        k = saved[0].shape[1]
+        outs, works, keep = [], [], []
+        for j in range(self.pipeline):  # part j's reduce-scatter beside part j+1's backward
+            rp, col, val = self.parts[j]
+            if col.numel() > 0:
+                partial = self.kernels.sspmm_backward(rp, col, val, g, saved[j],
+                                                      row_div=row_div_local,
+                                                      plan=self.plan(k, g.shape[1], j))
+            else:
+                partial = torch.zeros(self.n_cols_part, k, dtype=g.dtype, device=g.device)
+            o = torch.empty(self.vh, k, dtype=g.dtype, device=g.device)
+            works.append(reduce_scatter_rows(o, partial.contiguous(), self.group, async_op=True))
+            outs.append(o)
+            keep.append(partial)
+        for w in works:
+            _wait(w)
+        return torch.cat(outs)[:self.n_local]
 
     # ---- the two aggregation passes
     def forward(self, val_all, idx_all, D: int, row_div_local=None) -> torch.Tensor:
@@ -276,17 +392,21 @@ class ShardedMaxKFunction(Function):
     def forward(ctx, shard: ShardedMaxK, topk_values, topk_indices, dim_origin: int,
                 degrees_local=None):
         idx = topk_indices if topk_indices.dtype == torch.uint8 else topk_indices.to(torch.uint8)
-        val_all, idx_all = shard.gather_cbsr(topk_values.float().contiguous(), idx.contiguous())
+        y, saved = shard.aggregate(topk_values.float().contiguous(), idx.contiguous(),
+                                   dim_origin, degrees_local)
+        saved = saved if isinstance(saved, list) else [saved]
         ctx.shard = shard
-        ctx.save_for_backward(idx_all, degrees_local if degrees_local is not None
+        ctx.n_saved = len(saved)
+        ctx.save_for_backward(*saved, degrees_local if degrees_local is not None
                               else torch.empty(0))
         ctx.has_div = degrees_local is not None
-        return shard.forward(val_all, idx_all, dim_origin, degrees_local)
+        return y
 
     @staticmethod
     def backward(ctx, grad_output):
-        idx_all, deg = ctx.saved_tensors
-        g = ctx.shard.backward(grad_output.float(), idx_all, deg if ctx.has_div else None)
+        *saved, deg = ctx.saved_tensors
+        st = saved if ctx.shard.pipeline > 1 else saved[0]
+        g = ctx.shard.grad(grad_output.float(), st, deg if ctx.has_div else None)
         return None, g, None, None, None
 
 

@@ -29,11 +29,19 @@ BWD_ATOL = 1e-5
 class OracleKernels:
     """kernels= backend for ShardedMaxK built on the CPU oracle (tests only)."""
 
-    def spgemm_forward(self, indptr, indices, values, cbsr_val, cbsr_idx, D, row_div=None):
-        y = oracle.spgemm_fwd(indptr.numpy(), indices.numpy(), values.numpy(), cbsr_val.numpy(),
-                              cbsr_idx.numpy(), D,
-                              row_div=None if row_div is None else row_div.numpy())
-        return torch.from_numpy(y)
+    def spgemm_forward(self, indptr, indices, values, cbsr_val, cbsr_idx, D, row_div=None,
+                       out=None, accumulate=False):
+        y = torch.from_numpy(oracle.spgemm_fwd(indptr.numpy(), indices.numpy(), values.numpy(),
+                                               cbsr_val.numpy(), cbsr_idx.numpy(), D,
+                                               row_div=None if row_div is None
+                                               else row_div.numpy()))
+        if out is None:
+            return y
+        if accumulate:
+            out += y
+        else:
+            out.copy_(y)
+        return out
 
     def sspmm_backward(self, indptr, indices, values, grad, cbsr_idx, row_div=None, plan=None):
         g = oracle.sspmm_bwd(indptr.numpy(), indices.numpy(), values.numpy(), grad.numpy(),
@@ -63,7 +71,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gather"):
+def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gather",
+            pipeline=1):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -78,7 +87,8 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gat
 
         shard = maxk_dist.ShardedMaxK(torch.from_numpy(row_ptr), torch.from_numpy(col),
                                       torch.from_numpy(val), rank, world,
-                                      kernels=OracleKernels(), bounds=bounds, mode=mode)
+                                      kernels=OracleKernels(), bounds=bounds, mode=mode,
+                                      pipeline=pipeline)
         v0, v1 = shard.v0, shard.v1
         div = torch.from_numpy(deg[v0:v1]) if use_div else None
         val_l = torch.from_numpy(tv[v0:v1]).requires_grad_(True)
@@ -93,12 +103,14 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gat
         raise
 
 
-def _run(world, V=400, D=64, k=8, seed=0, use_div=True, bounds=None, mode="gather"):
+def _run(world, V=400, D=64, k=8, seed=0, use_div=True, bounds=None, mode="gather",
+         pipeline=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, V, D, k, seed, use_div, q, bounds, mode))
+                         args=(r, world, port, V, D, k, seed, use_div, q, bounds, mode,
+                               pipeline))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -122,21 +134,26 @@ def _single(V, D, k, seed, use_div):
     return y, gs
 
 
-@pytest.mark.parametrize("mode", ["gather", "halo", "auto"])
+@pytest.mark.parametrize("mode,pipeline", [("gather", 1), ("gather", 2), ("gather", 3),
+                                           ("halo", 1), ("auto", None)])
 @pytest.mark.parametrize("world,use_div,bounds", [(2, True, None), (3, False, None),
                                                   (4, True, None),
                                                   (3, True, [0, 150, 150, 400])])
-def test_sharded_matches_single_process(world, use_div, bounds, mode):
+def test_sharded_matches_single_process(world, use_div, bounds, mode, pipeline):
     """The last case gives rank 1 no rows: it still joins every collective (an all-padding
     chunk in "gather" mode, empty splits in "halo" mode), and the other ranks' results are
-    unchanged."""
+    unchanged.  pipeline > 1 ("gather"): the exchange in column parts, the forward summed
+    part by part (so within 1e-6 of the one-pass sum instead of bit-exact)."""
     V, D, k, seed = 400, 64, 8, 7
-    outs = _run(world, V, D, k, seed, use_div, bounds, mode)
+    outs = _run(world, V, D, k, seed, use_div, bounds, mode, pipeline)
     y_ref, gs_ref = _single(V, D, k, seed, use_div)
     covered = 0
     for rank, v0, v1, y, gs, bounds, xb, n_cols in outs:
         assert bounds[0] == 0 and bounds[-1] == V
-        np.testing.assert_array_equal(y, y_ref[v0:v1])
+        if pipeline == 1 or mode == "halo":
+            np.testing.assert_array_equal(y, y_ref[v0:v1])
+        else:
+            np.testing.assert_allclose(y, y_ref[v0:v1], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(gs, gs_ref[v0:v1], rtol=1e-5, atol=BWD_ATOL)
         covered += v1 - v0
     assert covered == V
@@ -219,7 +236,7 @@ def _local_worker(rank, world, port, args, D, k, q):
                          shard.n_cols)
         yg, gg, xg, _ = res["gather"]
         yh, gh, xh, nh = res["halo"]
-        np.testing.assert_array_equal(yh, yg)
+        np.testing.assert_allclose(yh, yg, rtol=1e-5, atol=1e-6)  # gather: pipelined parts
         np.testing.assert_allclose(gh, gg, rtol=1e-5, atol=BWD_ATOL)
         q.put((rank, v0, v1, yh, gh, shard.bounds, xh, nh, xg))
         dist.barrier()

@@ -65,6 +65,32 @@ def test_forward_golden(mk, cuda, path, chunk):
     close(y, z["y_ref"])
 
 
+@pytest.mark.parametrize("chunk", [0, 5, 37])
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_forward_accumulate_golden(mk, cuda, path, chunk):
+    """maxk_spgemm_forward_accumulate: the golden graph's edges split into two sub-CSRs by
+    column parity (the sharded forward's pipelined parts, maxk_dist); the first product
+    written, the second added onto it, must equal the whole graph's (small chunks cut hub
+    rows into slabs, whose fixup then adds onto the accumulated rows)."""
+    z = load_golden(path)
+    rp, col, val = z["row_ptr"], z["col_idx"], z["val"]
+    rows = np.repeat(np.arange(rp.size - 1), np.diff(rp))
+    parts = []
+    for par in (0, 1):
+        m = (col % 2) == par
+        rpj = np.zeros_like(rp)
+        rpj[1:] = np.cumsum(np.bincount(rows[m], minlength=rp.size - 1))
+        parts.append((T(rpj, cuda), T(col[m], cuda), T(val[m], cuda)))
+    args = (T(z["topk_val"], cuda), T(z["topk_idx"], cuda), int(z["D"]))
+    div = T(z["deg"], cuda)
+    y = mk.spgemm_forward(*parts[0], *args, row_div=div, chunk=chunk)
+    y2 = mk.spgemm_forward(*parts[1], *args, row_div=div, chunk=chunk, out=y, accumulate=True)
+    assert y2 is y
+    close(y, z["y_ref"])
+    with pytest.raises(RuntimeError):
+        mk.spgemm_forward(*parts[1], *args, accumulate=True)  # needs out=
+
+
 @pytest.mark.parametrize("mode", ["auto", "pull", "bucket", "csc", "atomic"])
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)

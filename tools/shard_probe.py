@@ -24,6 +24,10 @@ ap.add_argument("--k", type=int, default=None)
 ap.add_argument("--worlds", type=int, nargs="*", default=[1, 2, 4, 8])
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--reorder", action="store_true", help="relabel by maxk_graph.locality_order")
+ap.add_argument("--pipelines", type=int, nargs="*", default=[],
+                help="also time the pipelined gather mode's column parts (maxk_dist PIPELINE)")
+ap.add_argument("--busbw", type=float, nargs="*", default=[250.0, 375.0, 500.0],
+                help="RCCL all-gather / reduce-scatter bus bandwidths (GB/s) for the step model")
 a = ap.parse_args()
 P = maxk_graph.PRESETS[a.graph]
 k = a.k or P["k"]
@@ -84,3 +88,70 @@ for world in a.worlds:
     eff = f"  compute-only efficiency {base / (world * t):.2f}" if base and world > 1 else ""
     print(f"  N={world}: rank {worst[3]} fwd {worst[0]:.3f} + bwd {worst[1]:.3f} = {t:.3f} ms "
           f"({worst[2]} edges, bwd {worst[4]}){eff}", flush=True)
+
+
+def step_model(parts_f, parts_b, ag_bytes, rs_bytes, world, busbw):
+    """Step time (ms) of one rank: the forward's all-gathers queued back to back on the
+    communicator's stream, part j's product after its all-gather (j > 0 accumulating); the
+    backward's part j reduce-scatter after its backward, beside the next part's backward.
+    ag_bytes / rs_bytes: one part's whole collective size; a collective moves (N-1)/N of it
+    per rank at the bus bandwidth."""
+    P = len(parts_f)
+    a = ag_bytes * (world - 1) / world / (busbw * 1e6)
+    r = rs_bytes * (world - 1) / world / (busbw * 1e6)
+    t_ag = t_f = 0.0  # forward: end of the last all-gather and of the last product
+    for j in range(P):
+        t_ag += a
+        t_f = max(t_f, t_ag) + parts_f[j]
+    t_b = t_rs = 0.0  # backward
+    for j in range(P):
+        t_b += parts_b[j]
+        t_rs = max(t_rs, t_b) + r
+    return t_f + max(t_b, t_rs)
+
+
+if a.pipelines:
+    base_t = None
+    for world in [w for w in a.worlds if w > 1]:
+        for Pn in a.pipelines:
+            worst = None
+            for rank in range(world):
+                sh = maxk_dist.ShardedMaxK(row_ptr, col, val, rank, world, device=dev,
+                                           mode="gather", pipeline=Pn)
+                cv, ci = mk.topk_cbsr(X, k)
+                b, vh, Pr = sh.bounds, (sh.vh if sh.pipeline > 1 else sh.vmax), sh.pipeline
+                gl = G[sh.v0:sh.v1].contiguous()
+                y = torch.empty(sh.n_local, D, device=dev)
+                tf, tb = [], []
+                for j in range(Pr):
+                    cvj = torch.zeros(world * vh, k, device=dev)
+                    cij = torch.zeros(world * vh, k, dtype=torch.uint8, device=dev)
+                    for p in range(world):
+                        lo, hi = b[p] + j * vh, min(b[p] + (j + 1) * vh, b[p + 1])
+                        if hi > lo:
+                            cvj[p * vh:p * vh + hi - lo] = cv[lo:hi]
+                            cij[p * vh:p * vh + hi - lo] = ci[lo:hi]
+                    rp, cj, vj = sh.parts[j] if Pr > 1 else (sh.row_ptr, sh.col_idx, sh.values)
+                    nc = sh.n_cols_part if Pr > 1 else sh.n_cols
+                    tf.append(timed(lambda: mk.spgemm_forward(rp, cj, vj, cvj, cij, D, out=y,
+                                                              validate=False, accumulate=j > 0)))
+                    plan = sh.plan(k, D, j if Pr > 1 else None)
+                    mode = mk._bwd_mode(None, k, cj.numel(), nc, sh.n_local, D, (rp, cj))
+                    gs = torch.empty(nc, k, device=dev)
+                    tb.append(timed(lambda: mk.sspmm_backward(rp, cj, vj, gl, cij, out=gs,
+                                                              validate=False, mode=mode,
+                                                              plan=plan)))
+                    del cvj, cij, gs, plan
+                ag, rs = world * vh * k * 5, world * vh * k * 4
+                if worst is None or sum(tf) + sum(tb) > sum(worst[0]) + sum(worst[1]):
+                    worst = (tf, tb, ag, rs, rank)
+                del sh, gl, y
+            tf, tb, ag, rs, rk = worst
+            print(f"  N={world} pipeline {Pn}: slowest rank {rk}: fwd parts "
+                  f"{' + '.join(f'{x:.3f}' for x in tf)}, bwd parts "
+                  f"{' + '.join(f'{x:.3f}' for x in tb)} ms; per part all-gather {ag / 1e6:.1f} MB, "
+                  f"reduce-scatter {rs / 1e6:.1f} MB", flush=True)
+            for bw in a.busbw:
+                t = step_model(tf, tb, ag, rs, world, bw)
+                sp = f", {base / t:.2f}x over N=1" if base else ""
+                print(f"     busbw {bw:.0f} GB/s: step {t:.3f} ms{sp}", flush=True)
