@@ -459,6 +459,12 @@ def main():
     t_plan = time.perf_counter() - t_plan
 
     pipelined = world > 1 and shard.pipeline > 1
+    # csc backward: the forward writes each edge's selectors, phase 1 reads them in order
+    # (maxk_spgemm_forward_sel / maxk_sspmm_backward_csc_sel) where that pays: k <= 16 by
+    # default, MAXK_EDGE_SEL=0/1 off / on (mk.edge_selectors_wanted)
+    es = (torch.empty(El, k, dtype=torch.uint8, device=dev)
+          if (not pipelined and args.bwd_mode == "csc" and El > 0
+              and mk.edge_selectors_wanted(k)) else None)
     if pipelined:  # the parts' plans (per-graph setup, untimed), in the bench's backward mode
         shard.kernels.bwd_mode = args.bwd_mode
         t_plan = time.perf_counter()
@@ -483,14 +489,15 @@ def main():
             if world > 1:
                 cv_all, ci_all = shard.gather_cbsr(cv_loc[:nl], ci_loc[:nl])
             mk.spgemm_forward(l_row_ptr, l_col, l_val, cv_all, ci_all, D, out=y,
-                              chunk=args.chunk, validate=False)
+                              chunk=args.chunk, validate=False, edge_sel_out=es)
         if ev:
             ev[1].record()
         if pipelined:
             gs_loc[:nl] = shard.grad(l_G, saved)
         else:
             mk.sspmm_backward(l_row_ptr, l_col, l_val, l_G, ci_all, out=gs_all,
-                              chunk=args.chunk, validate=False, mode=args.bwd_mode, plan=plan)
+                              chunk=args.chunk, validate=False, mode=args.bwd_mode, plan=plan,
+                              edge_sel=es)
             if world > 1:
                 gs_loc[:nl] = shard.scatter_grad(gs_all)
         if ev:
@@ -570,7 +577,8 @@ def main():
         "fwd_alg_GBs": round(B_f / fwd_avg / 1e6, 1), "bwd_alg_GBs": round(B_b / bwd_avg / 1e6, 1),
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
         "bwd_mode": args.bwd_mode, "backward_plan_s": round(t_plan, 4),
-        "build_config": build_cfg, "fwd_compulsory_GBs": round(C_f / fwd_avg / 1e6, 1),
+        "build_config": build_cfg, "edge_sel_stream": es is not None,
+        "fwd_compulsory_GBs": round(C_f / fwd_avg / 1e6, 1),
         "bwd_compulsory_GBs": round(C_b / bwd_avg / 1e6, 1),
     }
     if args.reorder:

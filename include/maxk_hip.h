@@ -74,6 +74,16 @@ int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_idx, const fl
                         float *out, int64_t num_rows, int64_t num_cols, int64_t num_e,
                         int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
                         void *workspace, size_t workspace_bytes, void *stream);
+/* The same forward, also writing each edge's selectors: edge_sel[e, l] = cbsr_idx[col_idx[e], l]
+ * (u8 [num_e, k]), the stream maxk_sspmm_backward_csc_sel reads.  The forward gathers every
+ * edge's CBSR record anyway, so the stream costs one coalesced write of num_e * k bytes
+ * (tables past 2^24 columns or 4 GiB of records: a separate gather, maxk_edge_selectors). */
+int maxk_spgemm_forward_sel(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                            const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div,
+                            float *out, int64_t num_rows, int64_t num_cols, int64_t num_e,
+                            int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                            void *workspace, size_t workspace_bytes, void *stream,
+                            uint8_t *edge_sel);
 /* The same product added onto out (out += ...; out must hold valid values): a row range's
  * result summed over several column ranges of A, e.g. the sharded forward's pipelined halves
  * (maxk_dist.py), without a separate pass over out.  Same arguments and workspace. */
@@ -117,6 +127,23 @@ int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *col_idx, cons
                             int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
                             int32_t dim_k, int32_t chunk_edges, void *workspace,
                             size_t workspace_bytes, void *stream);
+
+/* The same csc backward with the selectors given per edge: edge_sel[num_e, k] (u8, 4-B
+ * aligned, dim_k % 4 == 0) with edge_sel[e, l] = cbsr_idx[col_idx[e], l].  Phase 1 then reads
+ * them in CSR order beside the weights instead of gathering a random cbsr_idx row (a whole
+ * 128-B line) per edge -- the step that bounds phase 1 on large sparse graphs.  A forward that
+ * gathered each edge's CBSR record anyway writes the stream for free
+ * (maxk_spgemm_forward_sel); maxk_edge_selectors builds it by a gather otherwise. */
+int maxk_sspmm_backward_csc_sel(const int32_t *row_ptr, const int32_t *col_idx,
+                                const float *edge_val, const float *grad_out, const float *row_div,
+                                const uint8_t *edge_sel, const int32_t *col_ptr,
+                                const int32_t *csc_eid, float *grad_cbsr, int64_t num_rows,
+                                int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                                int32_t chunk_edges, void *workspace, size_t workspace_bytes,
+                                void *stream);
+/* edge_sel[e, l] = cbsr_idx[col_idx[e], l] (dim_k % 4 == 0; both arrays 16-B aligned). */
+int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_idx, int64_t num_e,
+                        int32_t dim_k, uint8_t *edge_sel, void *stream);
 
 /* Transpose plan of a CSR graph (once per graph): col_ptr[num_cols+1] of the
  * CSC and csc_eid[num_e] = the CSR edge id held by CSC slot t (stable in CSR order).

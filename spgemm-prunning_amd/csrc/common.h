@@ -35,6 +35,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_FWD_WAVES
 #define MAXK_FWD_WAVES 1
 #endif
+#ifndef MAXK_FWD_EMIT_WAVES  // the forward emitting edge selectors: __launch_bounds__ minimum
+#define MAXK_FWD_EMIT_WAVES 1   // (workgroups per CU) -- a VGPR cap for its occupancy
+#endif
 #ifndef MAXK_BWD_WAVES
 #define MAXK_BWD_WAVES 1
 #endif

@@ -64,7 +64,11 @@ inline int fwd_lanes_per_edge(int k) {
 // k=32: 306k workgroups, 1.65 ms).  Duplicate selectors of a vertex: the first
 // occurrence (lowest l, found with an LDS atomicMin per (vertex, selector))
 // carries the sum of their values in l order, the others point at the trash
-// column `trash` with value 0.  Selectors >= D also go to trash.
+// column with value 0.  Selectors >= D also go to trash.  A record's u16 selector is the
+// selector itself when it is kept, else 0x100 | selector: the walkers take min(selector,
+// trash) as the LDS column (every index in [D, DS) is a never-flushed pad column of the copy),
+// and the low byte stays the caller's selector, which the edge-selector stream of
+// maxk_spgemm_forward_sel needs.
 constexpr int kPackMaxV = 32;     // vertices per group (LDS: 32 x 256 first-occurrence slots)
 constexpr int kPackBlock = 512;   // threads per pack workgroup (products: 0.34 -> 0.21 ms vs 256)
 
@@ -107,7 +111,7 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack_kernel(const float *__re
             const bool keep = first && s < D;
             uint8_t *p = rec + v * RS;
             reinterpret_cast<float *>(p)[l] = keep ? outv : 0.f;
-            reinterpret_cast<uint16_t *>(p + 4 * k)[l] = (uint16_t)(keep ? s : trash);
+            reinterpret_cast<uint16_t *>(p + 4 * k)[l] = (uint16_t)(keep ? s : (0x100 | s));
         }
         __syncthreads();  // LDS is reused by the next group
     }
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack4_kernel(const float *__r
                 }
                 const bool keep = first && (int)sj < D;
                 o[j] = keep ? o[j] : 0.f;
-                sel[j] = keep ? sj : (uint32_t)trash;
+                sel[j] = keep ? sj : (0x100u | sj);
             }
             uint8_t *p = rec + v * RS;
             *reinterpret_cast<float4 *>(p + 4 * l0) = make_float4(o[0], o[1], o[2], o[3]);
@@ -180,25 +184,61 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack4_kernel(const float *__r
     }
 }
 
-template <int KG, int U, bool WIDE>
+// EMIT (maxk_spgemm_forward_sel, k <= KG so one pass over l): every lane stores its edge's
+// selector byte to esel[e * k + l] -- a wave step's G edges x k bytes are one contiguous run.
+// The stores go one batch late, right after the next batch's column loads and before that
+// batch's waits: on gfx950 stores count in vmcnt with the loads, so a store issued right after
+// its own batch would make the next wait for loads wait for the store too, and one held past
+// the next record loads keeps its bytes live through the batch's peak register use.  They are
+// non-temporal (the stream must not push the record lines out of L2), and the pending bytes sit
+// four to a register with the batch position kept wave-uniform.
+template <int KG, int U, bool WIDE, bool EMIT = false>
 struct EdgeWalker {
     static constexpr int G = kWave / KG;  // edges per wave step
+
+    struct Pending {
+        uint32_t b[(U + 3) / 4];
+        int pos = -1;  // the pending batch's first edge offset (-1: none yet)
+        __device__ __forceinline__ void keep(int u, int sel) {
+            const uint32_t x = ((uint32_t)sel & 0xffu) << (8 * (u % 4));
+            b[u / 4] = u % 4 == 0 ? x : (b[u / 4] | x);
+        }
+        // step u of the pending batch is edge offset pos + u * ustride + lane_off (in the
+        // segment), stored when it is below lim and the lane's l below k
+        __device__ __forceinline__ void flush(__amdgpu_buffer_rsrc_t ers, int ustride, int lane_off,
+                                              int lim, int k, int l) const {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = pos + u * ustride + lane_off;
+                const int off = pos >= 0 && e < lim && l < k ? e * k + l : (int)0x80000000;
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(b[u / 4] >> (8 * (u % 4))), ers,
+                                                     off, 0, MAXK_T_AUX);
+            }
+        }
+    };
 
     // Short-row batch: group g (KG lanes) walks row g's edges [sb_g, se_g) alone, U at a
     // time, into its own copy acc_g; the rows are consecutive, so their edges are one
     // contiguous range [e0, e_end) and one descriptor covers every group.  Edges past a
     // group's row (the next row's, or past e_end: 0) go to the trash column with weight 0.
+    // esel (EMIT): each edge's selector bytes are stored to esel[e * k + l] on the way.
     __device__ __forceinline__ static void run_rows(float *acc_g, const int32_t *__restrict__ col_idx,
                                                     const float *__restrict__ edge_val,
                                                     const uint8_t *__restrict__ rec, int RS,
                                                     int e0, int e_end, int sb_g, int len_g,
-                                                    int n_it, int k, int trash, int lane) {
+                                                    int n_it, int k, int trash, int lane,
+                                                    uint8_t *__restrict__ esel) {
         const int l0 = lane % KG;
         const int n = e_end - e0;  // wave-uniform
         const auto crs = wave_buffer(col_idx + e0, (uint32_t)n * 4u);
         const auto vrs = wave_buffer(edge_val + e0, (uint32_t)n * 4u);
         const auto rrs = wave_buffer(rec, 0xffffffffu);
         const int lo = (sb_g - e0) * 4;
+        const auto ers = wave_buffer(EMIT ? esel + (size_t)(uint32_t)e0 * k : nullptr,
+                                     EMIT ? (uint32_t)n * (uint32_t)k : 0u);
+        // EMIT: group g's edge j (its row's j-th) sits at offset sb_g - e0 + j of the range;
+        // stored right away (a short-row batch is one or two iterations: nothing to lag)
+        const int g_off = sb_g - e0;
         for (int it = 0; it < n_it; ++it) {
             int c[U];
             float w[U];
@@ -225,7 +265,12 @@ struct EdgeWalker {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     const bool live = lok && it * U + u < len_g;
-                    acc_g[live ? s[u] : trash] += w[u] * v[u];
+                    float *a = &acc_g[live ? min(s[u], trash) : trash];
+                    *a = __builtin_fmaf(w[u], v[u], *a);  // one rounding, in every variant
+                    if constexpr (EMIT)
+                        __builtin_amdgcn_raw_buffer_store_b8(
+                            (uint8_t)s[u], ers, live ? (g_off + it * U + u) * k + l : (int)0x80000000,
+                            0, MAXK_T_AUX);
                 }
             }
         }
@@ -244,7 +289,8 @@ struct EdgeWalker {
     __device__ __forceinline__ static void run(float *acc_g, const int32_t *__restrict__ col_idx,
                                                const float *__restrict__ edge_val,
                                                const uint8_t *__restrict__ rec, int RS, int sb,
-                                               int se, int k, int trash, int lane) {
+                                               int se, int k, int trash, int lane,
+                                               uint8_t *__restrict__ esel) {
         const int grp = lane / KG;
         const int l0 = lane % KG;
         if constexpr (!WIDE) {
@@ -252,6 +298,10 @@ struct EdgeWalker {
             const auto crs = wave_buffer(col_idx + sb, (uint32_t)n * 4u);
             const auto vrs = wave_buffer(edge_val + sb, (uint32_t)n * 4u);
             const auto rrs = wave_buffer(rec, 0xffffffffu);  // offsets < num_cols * RS < 2^32
+            // EMIT: the segment's edge-selector rows
+            const auto ers = wave_buffer(EMIT ? esel + (size_t)(uint32_t)sb * k : nullptr,
+                                         EMIT ? (uint32_t)n * (uint32_t)k : 0u);
+            Pending pend;
             for (int base = 0; base < n; base += G * U) {
                 int c[U];
                 float w[U];
@@ -261,6 +311,10 @@ struct EdgeWalker {
                     c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
                     w[u] = __uint_as_float(
                         __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
+                }
+                if constexpr (EMIT) {
+                    pend.flush(ers, G, grp, n, k, l0);
+                    __builtin_amdgcn_sched_barrier(0);  // the stores stay ahead of the record loads
                 }
                 for (int lb = 0; lb < k; lb += KG) {  // one pass unless k > 64
                     const int l = lb + l0;
@@ -279,10 +333,14 @@ struct EdgeWalker {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const bool live = lok && base + u * G + grp < n;
-                        acc_g[live ? s[u] : trash] += w[u] * v[u];
+                        float *a = &acc_g[live ? min(s[u], trash) : trash];
+                        *a = __builtin_fmaf(w[u], v[u], *a);  // one rounding, in every variant
+                        if constexpr (EMIT) pend.keep(u, s[u]);
                     }
+                    if constexpr (EMIT) pend.pos = base;
                 }
             }
+            if constexpr (EMIT) pend.flush(ers, G, grp, n, k, l0);
         } else {
             const int last = se - 1;
             for (int base = sb; base < se; base += G * U) {
@@ -309,7 +367,10 @@ struct EdgeWalker {
                         s[u] = reinterpret_cast<const uint16_t *>(p + 4 * k)[lc];
                     }
 #pragma unroll
-                    for (int u = 0; u < U; ++u) acc_g[lok ? s[u] : trash] += w[u] * v[u];
+                    for (int u = 0; u < U; ++u) {
+                        float *a = &acc_g[lok ? min(s[u], trash) : trash];
+                        *a = __builtin_fmaf(w[u], v[u], *a);
+                    }
                 }
             }
         }
@@ -365,13 +426,13 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
     wave_lds_fence();
 }
 
-template <int KG, int U, bool WIDE>
-__global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
+template <int KG, int U, bool WIDE, bool EMIT>
+__global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
     const float *__restrict__ edge_val, const uint8_t *__restrict__ rec, int RS,
     const float *__restrict__ row_div, float *__restrict__ out, float *__restrict__ slab,
     int32_t *__restrict__ slab_row, int num_rows, int64_t num_e, int D, int DS, int k,
-    int chunk, int n_items, int accumulate) {
+    int chunk, int n_items, int accumulate, uint8_t *__restrict__ esel) {
     constexpr int NC = kWave / KG;  // LDS copies per wave (one per edge group)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wid = threadIdx.x / kWave;
@@ -399,8 +460,8 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
         if (d1 - r < se) se = d1 - r;
         if (sb < se) {
             wave_lds_fence();
-            EdgeWalker<KG, U, WIDE>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se, k, DS - 1,
-                                   lane);
+            EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se,
+                                               k, DS - 1, lane, esel);
             const float div = row_div ? row_div[r - 1] : 1.f;
             flush_row<NC>(acc, DS, slab + (int64_t)item * D, D, div, row_div != nullptr, lane);
             cont = r - 1;
@@ -411,12 +472,12 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     // Rows whose token lies in [d0, d1): this item owns them.  row_ptr of 64 consecutive rows
     // sits one per lane (window from row wb), for the short-row test below.
     int wb = r, rpw = 0;
-    if constexpr (NC > 1 && !WIDE && MAXK_FWD_SHORT > 0)
+    if constexpr (NC > 1 && !WIDE && !EMIT && MAXK_FWD_SHORT > 0)
         rpw = row_ptr[r + lane <= num_rows ? r + lane : num_rows];
     while (r < num_rows) {
         const int64_t rb = row_ptr[r];
         if (rb + r >= d1) break;
-        if constexpr (NC > 1 && !WIDE && MAXK_FWD_SHORT > 0) {
+        if constexpr (NC > 1 && !WIDE && !EMIT && MAXK_FWD_SHORT > 0) {
             // Short-row batch: up to NC consecutive rows, each wholly inside the item and at
             // most MAXK_FWD_SHORT edges long, one per lane group, so a wave keeps NC rows'
             // loads in flight instead of walking one short row at a time (Flickr: avg
@@ -444,9 +505,9 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
                     maxlen = lj > maxlen ? lj : maxlen;
                 }
                 wave_lds_fence();
-                EdgeWalker<KG, U, WIDE>::run_rows(acc_g, col_idx, edge_val, rec, RS, e0, e_end,
-                                                  sb_g, len_g, (maxlen + U - 1) / U, k, DS - 1,
-                                                  lane);
+                EdgeWalker<KG, U, WIDE, EMIT>::run_rows(acc_g, col_idx, edge_val, rec, RS, e0,
+                                                        e_end, sb_g, len_g, (maxlen + U - 1) / U,
+                                                        k, DS - 1, lane, esel);
                 for (int j = 0; j < m; ++j) {
                     const float div = row_div ? row_div[r + j] : 1.f;
                     flush_row<1>(acc + j * DS, DS, out + (int64_t)(r + j) * D, D, div,
@@ -460,8 +521,8 @@ __global__ __launch_bounds__(kBlock, MAXK_FWD_WAVES) void spgemm_fwd_kernel(
         if (d1 - r - 1 < se) se = d1 - r - 1;
         wave_lds_fence();
         if (rb < se)
-            EdgeWalker<KG, U, WIDE>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se, k, DS - 1,
-                                   lane);
+            EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se,
+                                               k, DS - 1, lane, esel);
         const float div = row_div ? row_div[r] : 1.f;
         flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane,
                       accumulate != 0);
@@ -509,7 +570,7 @@ template <int KG>
 void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 const float *edge_val, const uint8_t *rec, const float *row_div, float *out,
                 float *slab, int32_t *slab_row, int num_rows, int64_t num_e, int D, int k,
-                int accumulate) {
+                int accumulate, uint8_t *esel) {
     constexpr int U = MAXK_FWD_U;
     constexpr int NC = kWave / KG;
     const size_t lds = (size_t)kWavesPerBlock * NC * L.DS * sizeof(float);
@@ -517,14 +578,19 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
     const dim3 grid((unsigned)(MAXK_FWD_XCD ? xcd_grid(blocks) : blocks));
     // 32-bit record offsets need c < 2^24 (24-bit multiply) and the table under 4 GiB
     const int64_t num_cols = (int64_t)(L.rec_bytes / L.RS);
-    if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32))
-        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false>), grid, dim3(kBlock), lds, s, row_ptr,
-                           col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows,
-                           num_e, D, L.DS, k, L.chunk, L.n_items, accumulate);
+    // esel needs the buffer-descriptor path (the caller checks fwd_can_emit)
+    if (esel)
+        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, true>), grid, dim3(kBlock), lds, s,
+                           row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
+                           num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, esel);
+    else if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32))
+        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, false>), grid, dim3(kBlock), lds, s,
+                           row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
+                           num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, nullptr);
     else
-        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, true>), grid, dim3(kBlock), lds, s, row_ptr,
-                           col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row, num_rows,
-                           num_e, D, L.DS, k, L.chunk, L.n_items, accumulate);
+        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, true, false>), grid, dim3(kBlock), lds, s,
+                           row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
+                           num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, nullptr);
 }
 
 }  // namespace
@@ -544,7 +610,7 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
                  const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div, float *out,
                  int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
                  int32_t dim_k, int32_t chunk_edges, void *workspace, size_t workspace_bytes,
-                 void *stream, int accumulate) {
+                 void *stream, int accumulate, uint8_t *esel = nullptr) {
     MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range: %lld",
                  (long long)num_rows);
     MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
@@ -594,7 +660,7 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
 #define MAXK_CASE(KGV)                                                                     \
     case KGV:                                                                              \
         launch_fwd<KGV>(L, s, row_ptr, col_idx, edge_val, rec, row_div, out, slab,         \
-                        slab_row, nr, num_e, D, k, accumulate);                            \
+                        slab_row, nr, num_e, D, k, accumulate, esel);                      \
         break;
         MAXK_CASE(8)
         MAXK_CASE(16)
@@ -620,6 +686,26 @@ extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_id
     return forward_impl(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out, num_rows,
                         num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
                         workspace_bytes, stream, 0);
+}
+
+extern "C" int maxk_spgemm_forward_sel(const int32_t *row_ptr, const int32_t *col_idx,
+                                       const float *edge_val, const float *cbsr_val,
+                                       const uint8_t *cbsr_idx, const float *row_div, float *out,
+                                       int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                       int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                                       void *workspace, size_t workspace_bytes, void *stream,
+                                       uint8_t *edge_sel) {
+    clear_error();
+    MAXK_REQUIRE(num_e == 0 || edge_sel, "edge_sel must not be NULL");
+    const bool direct = dim_k <= kWave && num_cols < (1 << 24) &&
+                        (uint64_t)record_stride(dim_k, num_cols) * (uint64_t)num_cols < (1ull << 32);
+    if (int rc = forward_impl(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out,
+                              num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
+                              workspace_bytes, stream, 0, direct ? edge_sel : nullptr))
+        return rc;
+    if (direct || num_e == 0) return MAXK_OK;
+    // past 32-bit record offsets the walker takes 64-bit addresses and does not emit: gather
+    return maxk_edge_selectors(col_idx, cbsr_idx, num_e, dim_k, edge_sel, stream);
 }
 
 extern "C" int maxk_spgemm_forward_accumulate(const int32_t *row_ptr, const int32_t *col_idx,

@@ -32,7 +32,7 @@
 namespace maxk {
 namespace {
 
-enum { kAtomic = 0, kStore = 1, kStoreX4 = 2, kStoreX4W = 3 };
+enum { kAtomic = 0, kStore = 1, kStoreX4 = 2, kStoreX4W = 3, kStoreX4S = 4 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -50,11 +50,17 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 //    hardware drops the store, so no store is predicated.
 // Cache policy of the T stores: MAXK_T_AUX (0 plain, 2 nt, 16 sc1).  Store lag as in
 // push_edges below.
-template <int LR, int U, bool WIDE>
+// ES (edge selectors, maxk_sspmm_backward_csc_sel): the selectors come as a per-edge stream
+// esel[e * k + l] (= cbsr_idx[col_idx[e], l]) read in CSR order beside the weights, instead
+// of a gather of the destination's row of cbsr_idx per edge: no column loads and no random
+// selector line per edge (an ogbn-products-sized table is 20-80 MB, and each gather moved a
+// whole 128-B line from the Infinity Cache).
+template <int LR, int U, bool WIDE, bool ES = false>
 __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__restrict__ col_idx,
                                         const float *__restrict__ edge_val,
                                         const uint8_t *__restrict__ cbsr_idx,
-                                        float *__restrict__ T, int sb, int se, int k, int lane) {
+                                        float *__restrict__ T, int sb, int se, int k, int lane,
+                                        const uint8_t *__restrict__ esel = nullptr) {
     constexpr int G = kWave / LR;
     constexpr int GU = G * U;
     const int grp = lane / LR;
@@ -63,7 +69,9 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
     const int n = se - sb;  // wave-uniform, <= chunk
     const auto crs = wave_buffer(col_idx + sb, (uint32_t)n * 4u);
     const auto vrs = wave_buffer(edge_val + sb, (uint32_t)n * 4u);
-    const auto srs = wave_buffer(cbsr_idx, 0xffffffffu);  // offsets < num_cols*k < 2^31
+    // ES: the segment's selector stream; else the table (offsets < num_cols*k < 2^31)
+    const auto srs = ES ? wave_buffer(esel + (size_t)(uint32_t)sb * k, (uint32_t)n * k)
+                        : wave_buffer(cbsr_idx, 0xffffffffu);
     const auto trs = wave_buffer(T + (size_t)(uint32_t)sb * k, (uint32_t)n * k * 4u);  // <= 2 MiB
     const uint32_t qsel = 4u * (uint32_t)(q < k4 ? q : k4 - 1);
     const uint32_t qst = q < k4 ? 16u * q : 0x80000000u;  // store offset term; past the end if idle
@@ -79,7 +87,7 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
         const int lo = grp * 4;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+            if (!ES) c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
             w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
         }
     }
@@ -94,7 +102,8 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
             const int lo = (base + GU + grp) * 4;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                cn[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+                if (!ES)
+                    cn[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
                 wn[u] = __uint_as_float(
                     __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
             }
@@ -102,7 +111,9 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
         uint32_t sv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            sv[u] = __builtin_amdgcn_raw_buffer_load_b32(srs, sel_off(c[u]), 0, 0);
+            sv[u] = __builtin_amdgcn_raw_buffer_load_b32(
+                srs, ES ? (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel)
+                        : sel_off(c[u]), 0, 0);
         if (pending && (MAXK_BWD_ABL & 8)) {  // tuning: scattered whole-row stores
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -131,7 +142,7 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
         if (!has_next) break;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            c[u] = cn[u];
+            if (!ES) c[u] = cn[u];
             w[u] = wn[u];
         }
     }
@@ -165,7 +176,12 @@ __device__ __forceinline__ void push_edges(const float *g_lds, const int32_t *__
                                            const float *__restrict__ edge_val,
                                            const uint8_t *__restrict__ cbsr_idx,
                                            float *__restrict__ dst, int dummy, int sb, int se,
-                                           int k, int lane) {
+                                           int k, int lane, const uint8_t *__restrict__ esel) {
+    if constexpr (MODE == kStoreX4S) {
+        push_x4<KG, U, false, true>(g_lds, col_idx, edge_val, cbsr_idx, dst, sb, se, k, lane,
+                                    esel);
+        return;
+    }
     if constexpr (MODE == kStoreX4 || MODE == kStoreX4W) {
         push_x4<KG, U, MODE == kStoreX4W>(g_lds, col_idx, edge_val, cbsr_idx, dst, sb, se, k, lane);
         return;
@@ -266,7 +282,8 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
     const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
     const float *__restrict__ edge_val, const float *__restrict__ grad,
     const float *__restrict__ row_div, const uint8_t *__restrict__ cbsr_idx,
-    float *__restrict__ dst, int num_rows, int64_t num_e, int D, int k, int chunk, int n_items) {
+    float *__restrict__ dst, int num_rows, int64_t num_e, int D, int k, int chunk, int n_items,
+    const uint8_t *__restrict__ esel) {
     __shared__ __attribute__((aligned(16))) float lds[kWavesPerBlock][kMaxDim];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
@@ -327,7 +344,7 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
         }
         wave_lds_fence();
         push_edges<KG, U, MODE>(g_lds, col_idx, edge_val, cbsr_idx, dst, (int)num_e, (int)sb64,
-                                (int)se64, k, lane);
+                                (int)se64, k, lane, esel);
     }
 }
 
@@ -1240,33 +1257,35 @@ template <int MODE>
 int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 const float *edge_val, const float *grad, const float *row_div,
                 const uint8_t *cbsr_idx, float *dst, int nr, int64_t num_cols, int64_t num_e,
-                int D, int k, int chunk) {
+                int D, int k, int chunk, const uint8_t *esel = nullptr) {
     const int n_items = n_items_for(nr, num_e, chunk);
     const int64_t blocks = ceil_div(n_items, kWavesPerBlock);
     const dim3 grid((unsigned)(MAXK_P1_XCD ? xcd_grid(blocks) : blocks));
-    if (MODE == kStore && MAXK_BWD_X4 && k % 4 == 0) {
+    if (MODE == kStore && ((MAXK_BWD_X4 && k % 4 == 0) || esel)) {
         const int lr = lanes_per_edge(k / 4);
         const int u = MAXK_X4_U > 0 ? MAXK_X4_U : pick_depth(num_e, nr, kWave / lr, 4, 16);
         const bool wide = num_cols >= (1 << 24);  // selector offsets need a 32-bit multiply
         switch (lr) {
-#define MAXK_CASE(LRV)                                                                       \
-    case LRV:                                                                                \
-        if (wide)                                                                            \
-            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 8, kStoreX4W>), grid, dim3(kBlock), 0, \
-                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
-                               nr, num_e, D, k, chunk, n_items);                             \
-        else if (u <= 4)                                                                     \
-            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 4, kStoreX4>), grid, dim3(kBlock), 0,  \
-                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
-                               nr, num_e, D, k, chunk, n_items);                             \
-        else if (u <= 8)                                                                     \
-            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 8, kStoreX4>), grid, dim3(kBlock), 0,  \
-                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
-                               nr, num_e, D, k, chunk, n_items);                             \
-        else                                                                                 \
-            hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, 16, kStoreX4>), grid, dim3(kBlock), 0, \
-                               s, row_ptr, col_idx, edge_val, grad, row_div, cbsr_idx, dst,  \
-                               nr, num_e, D, k, chunk, n_items);                             \
+#define MAXK_GO(LRV, UV, MV)                                                                 \
+    hipLaunchKernelGGL((sspmm_bwd_kernel<LRV, UV, MV>), grid, dim3(kBlock), 0, s, row_ptr,   \
+                       col_idx, edge_val, grad, row_div, cbsr_idx, dst, nr, num_e, D, k,     \
+                       chunk, n_items, esel)
+#define MAXK_CASE(LRV)                          \
+    case LRV:                                   \
+        if (esel && u <= 4)                     \
+            MAXK_GO(LRV, 4, kStoreX4S);         \
+        else if (esel && u <= 8)                \
+            MAXK_GO(LRV, 8, kStoreX4S);         \
+        else if (esel)                          \
+            MAXK_GO(LRV, 16, kStoreX4S);        \
+        else if (wide)                          \
+            MAXK_GO(LRV, 8, kStoreX4W);         \
+        else if (u <= 4)                        \
+            MAXK_GO(LRV, 4, kStoreX4);          \
+        else if (u <= 8)                        \
+            MAXK_GO(LRV, 8, kStoreX4);          \
+        else                                    \
+            MAXK_GO(LRV, 16, kStoreX4);         \
         break;
             MAXK_CASE(1)
             MAXK_CASE(2)
@@ -1276,6 +1295,7 @@ int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
             MAXK_CASE(32)
             MAXK_CASE(64)
 #undef MAXK_CASE
+#undef MAXK_GO
             default:
                 set_error("unsupported lane group");
                 return MAXK_ERR_INVALID;
@@ -1288,7 +1308,7 @@ int launch_push(hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
     case KGV:                                                                                 \
         hipLaunchKernelGGL((sspmm_bwd_kernel<KGV, (KGV >= 8 ? MAXK_BWD_U : 4), MODE>), grid,  \
                            dim3(kBlock), 0, s, row_ptr, col_idx, edge_val, grad, row_div,     \
-                           cbsr_idx, dst, nr, num_e, D, k, chunk, n_items);                   \
+                           cbsr_idx, dst, nr, num_e, D, k, chunk, n_items, nullptr);          \
         break;
         MAXK_CASE(1)
         MAXK_CASE(2)
@@ -1382,21 +1402,22 @@ extern "C" size_t maxk_sspmm_backward_csc_workspace_size(int64_t num_rows, int64
     return csc_layout(num_cols, num_e, dim_k, chunk_edges).total;
 }
 
-extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *col_idx,
-                                       const float *edge_val, const float *grad_out,
-                                       const float *row_div, const uint8_t *cbsr_idx,
-                                       const int32_t *col_ptr, const int32_t *csc_eid,
-                                       float *grad_cbsr, int64_t num_rows, int64_t num_cols,
-                                       int64_t num_e, int32_t dim_origin, int32_t dim_k,
-                                       int32_t chunk_edges, void *workspace,
-                                       size_t workspace_bytes, void *stream) {
-    clear_error();
+namespace maxk {
+namespace {
+// edge_sel (k % 4 == 0): phase 1 reads each edge's selectors from this per-edge stream instead
+// of gathering them from cbsr_idx (push_x4, ES).
+int csc_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+             const float *grad_out, const float *row_div, const uint8_t *cbsr_idx,
+             const uint8_t *edge_sel, const int32_t *col_ptr, const int32_t *csc_eid,
+             float *grad_cbsr, int64_t num_rows, int64_t num_cols, int64_t num_e,
+             int32_t dim_origin, int32_t dim_k, int32_t chunk_edges, void *workspace,
+             size_t workspace_bytes, void *stream) {
     if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges)) return rc;
     hipStream_t s = as_stream(stream);
     if (num_cols == 0) return MAXK_OK;
     MAXK_REQUIRE(grad_cbsr && col_ptr, "grad_cbsr/col_ptr must not be NULL");
-    MAXK_REQUIRE(num_e == 0 || (row_ptr && col_idx && edge_val && grad_out && cbsr_idx &&
-                                csc_eid),
+    MAXK_REQUIRE(num_e == 0 || (row_ptr && col_idx && edge_val && grad_out &&
+                                (cbsr_idx || edge_sel) && csc_eid),
                  "CSR/grad/selector/transpose pointers must not be NULL");
     const CscLayout L = csc_layout(num_cols, num_e, dim_k, chunk_edges);
     MAXK_REQUIRE(workspace && workspace_bytes >= L.total,
@@ -1410,7 +1431,8 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
         if (int rc = launch_push<kStore>(s, row_ptr, col_idx, edge_val, grad_out, row_div,
                                          cbsr_idx, T, (int)num_rows, num_cols, num_e,
                                          dim_origin, k,
-                                         bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS)))
+                                         bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS),
+                                         edge_sel))
             return rc;
     }
     const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
@@ -1467,6 +1489,75 @@ extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *co
     }
     MAXK_LAUNCHED("csc_sum_kernel");
     return launch_slab_fixup<1>(slab, slab_row, grad_cbsr, k, L.n_items, s);
+}
+
+// edge_sel[e * k + l] = cbsr_idx[col_idx[e] * k + l]: 16 B per thread (k % 16 == 0), else 4 B
+__global__ __launch_bounds__(kBlock) void edge_sel_kernel(const int32_t *__restrict__ col_idx,
+                                                          const uint8_t *__restrict__ cbsr_idx,
+                                                          uint8_t *__restrict__ edge_sel,
+                                                          int64_t n_words, int k, int wb) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n_words) return;
+    const int wpe = k / wb;  // words per edge
+    const int64_t e = i / wpe;
+    const int w = (int)(i % wpe);
+    const size_t src = (size_t)(uint32_t)col_idx[e] * k + (size_t)w * wb;
+    if (wb == 16)
+        reinterpret_cast<uint4 *>(edge_sel)[i] = *reinterpret_cast<const uint4 *>(cbsr_idx + src);
+    else
+        reinterpret_cast<uint32_t *>(edge_sel)[i] = *reinterpret_cast<const uint32_t *>(cbsr_idx + src);
+}
+}  // namespace
+}  // namespace maxk
+
+extern "C" int maxk_sspmm_backward_csc(const int32_t *row_ptr, const int32_t *col_idx,
+                                       const float *edge_val, const float *grad_out,
+                                       const float *row_div, const uint8_t *cbsr_idx,
+                                       const int32_t *col_ptr, const int32_t *csc_eid,
+                                       float *grad_cbsr, int64_t num_rows, int64_t num_cols,
+                                       int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                                       int32_t chunk_edges, void *workspace,
+                                       size_t workspace_bytes, void *stream) {
+    clear_error();
+    MAXK_REQUIRE(num_e == 0 || cbsr_idx, "cbsr_idx must not be NULL");
+    return csc_impl(row_ptr, col_idx, edge_val, grad_out, row_div, cbsr_idx, nullptr, col_ptr,
+                    csc_eid, grad_cbsr, num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges,
+                    workspace, workspace_bytes, stream);
+}
+
+extern "C" int maxk_sspmm_backward_csc_sel(const int32_t *row_ptr, const int32_t *col_idx,
+                                           const float *edge_val, const float *grad_out,
+                                           const float *row_div, const uint8_t *edge_sel,
+                                           const int32_t *col_ptr, const int32_t *csc_eid,
+                                           float *grad_cbsr, int64_t num_rows, int64_t num_cols,
+                                           int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                                           int32_t chunk_edges, void *workspace,
+                                           size_t workspace_bytes, void *stream) {
+    clear_error();
+    MAXK_REQUIRE(dim_k % 4 == 0, "edge selectors need dim_k %% 4 == 0, got %d", dim_k);
+    MAXK_REQUIRE(num_e == 0 || edge_sel, "edge_sel must not be NULL");
+    MAXK_REQUIRE(((uintptr_t)edge_sel & 3) == 0, "edge_sel must be 4-B aligned");
+    return csc_impl(row_ptr, col_idx, edge_val, grad_out, row_div, nullptr, edge_sel, col_ptr,
+                    csc_eid, grad_cbsr, num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges,
+                    workspace, workspace_bytes, stream);
+}
+
+extern "C" int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_idx,
+                                   int64_t num_e, int32_t dim_k, uint8_t *edge_sel, void *stream) {
+    clear_error();
+    MAXK_REQUIRE(dim_k >= 4 && dim_k % 4 == 0 && dim_k <= kMaxDim,
+                 "edge selectors need dim_k %% 4 == 0, got %d", dim_k);
+    MAXK_REQUIRE(num_e >= 0 && num_e * (int64_t)dim_k < (1LL << 40), "num_e out of range");
+    if (num_e == 0) return MAXK_OK;
+    MAXK_REQUIRE(col_idx && cbsr_idx && edge_sel, "pointers must not be NULL");
+    MAXK_REQUIRE(((uintptr_t)edge_sel & 15) == 0 && ((uintptr_t)cbsr_idx & 15) == 0,
+                 "edge_sel / cbsr_idx must be 16-B aligned");
+    const int wb = dim_k % 16 == 0 ? 16 : 4;
+    const int64_t n_words = num_e * (dim_k / wb);
+    hipLaunchKernelGGL(edge_sel_kernel, dim3((unsigned)ceil_div(n_words, kBlock)), dim3(kBlock), 0,
+                       as_stream(stream), col_idx, cbsr_idx, edge_sel, n_words, dim_k, wb);
+    MAXK_LAUNCHED("edge_sel_kernel");
+    return MAXK_OK;
 }
 
 // Bucketed phase 2: entries per part (~MAXK_BUCKET_PARTS parts per CU, at least 16384).

@@ -199,9 +199,12 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                    cbsr_val: torch.Tensor, cbsr_idx: torch.Tensor, dim_origin: int,
                    row_div: Optional[torch.Tensor] = None, chunk: int = 0,
                    out: Optional[torch.Tensor] = None, validate: Optional[bool] = None,
-                   accumulate: bool = False) -> torch.Tensor:
+                   accumulate: bool = False, edge_sel_out: Optional[torch.Tensor] = None
+                   ) -> torch.Tensor:
     """out[num_rows, D] = diag(1/row_div) . A . scatter(cbsr)  (CSR A: indptr/indices/values).
-    accumulate: out += the product instead (out= required; maxk_spgemm_forward_accumulate)."""
+    accumulate: out += the product instead (out= required; maxk_spgemm_forward_accumulate).
+    edge_sel_out (uint8 [E, k]): also store each edge's selectors, cbsr_idx[indices[e]], for
+    sspmm_backward(..., edge_sel=) (maxk_spgemm_forward_sel)."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32), (cbsr_val, "input_data", torch.float32),
                      (cbsr_idx, "sparse_selector", torch.uint8)):
@@ -231,6 +234,18 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     E = indices.numel()
     ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, num_cols, E, D, k, chunk)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if edge_sel_out is not None:
+        if accumulate:
+            raise RuntimeError("edge_sel_out and accumulate cannot be combined")
+        _need(edge_sel_out, "edge_sel_out", torch.uint8)
+        if tuple(edge_sel_out.shape) != (E, k):
+            raise RuntimeError("edge_sel_out must be [num_e, k]")
+        with torch.cuda.device(dev):
+            _capi.check(L.maxk_spgemm_forward_sel(
+                _ptr(indptr), _ptr(indices), _ptr(values), _ptr(cbsr_val), _ptr(cbsr_idx),
+                _ptr(row_div), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws),
+                ws.numel(), _stream(dev), _ptr(edge_sel_out)), "maxk_spgemm_forward_sel")
+        return out
     fn = L.maxk_spgemm_forward_accumulate if accumulate else L.maxk_spgemm_forward
     with torch.cuda.device(dev):
         _capi.check(fn(
@@ -603,8 +618,12 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                    grad_output: torch.Tensor, cbsr_idx: torch.Tensor,
                    row_div: Optional[torch.Tensor] = None, chunk: int = 0,
                    out: Optional[torch.Tensor] = None, validate: Optional[bool] = None,
-                   mode: Optional[str] = None, plan=None) -> torch.Tensor:
+                   mode: Optional[str] = None, plan=None,
+                   edge_sel: Optional[torch.Tensor] = None) -> torch.Tensor:
     """grad_cbsr[num_cols, k] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]].
+
+    edge_sel (uint8 [E, k], k % 4 == 0; mode "csc", ignored by the others): the selectors per
+    edge (edge_selectors(), or the forward's by-product), read in CSR order instead of gathered.
 
     mode "auto" (default; MAXK_BWD_MODE overrides): "pull", "hybrid" or "csc", see _bwd_mode.
     mode "pull": per tile (row slice, destination bucket), the k values of every edge
@@ -734,11 +753,64 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     col_ptr, csc_eid = plan if plan is not None else transpose_plan(indices, num_cols)
     ws_bytes = L.maxk_sspmm_backward_csc_workspace_size(num_rows, num_cols, E, D, k, chunk)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    if edge_sel is not None:
+        _need(edge_sel, "edge_sel", torch.uint8)
+        if tuple(edge_sel.shape) != (E, k):
+            raise RuntimeError("edge_sel must be [num_e, k]")
+        with torch.cuda.device(dev):
+            _capi.check(L.maxk_sspmm_backward_csc_sel(
+                _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
+                _ptr(edge_sel), _ptr(col_ptr), _ptr(csc_eid), _ptr(out), num_rows, num_cols, E,
+                D, k, chunk, _ptr(ws), ws.numel(), _stream(dev)), "maxk_sspmm_backward_csc_sel")
+        return out
     with torch.cuda.device(dev):
         _capi.check(L.maxk_sspmm_backward_csc(
             _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
             _ptr(cbsr_idx), _ptr(col_ptr), _ptr(csc_eid), _ptr(out), num_rows, num_cols, E, D,
             k, chunk, _ptr(ws), ws.numel(), _stream(dev)), "maxk_sspmm_backward_csc")
+    return out
+
+
+EDGE_SEL_KMAX = 16
+
+
+def edge_selectors_wanted(k: int) -> bool:
+    """The rule for the per-edge selector stream given a csc backward: k % 4 == 0 and
+    k <= EDGE_SEL_KMAX by default (MAXK_EDGE_SEL=auto); MAXK_EDGE_SEL=0 never, =1 at every
+    k % 4 == 0.  Measured on the ogbn-products-sized graph: the forward that
+    writes the stream takes +0.68 / +0.80 / +1.14 ms at k = 8 / 16 / 32, the csc backward that
+    reads it -1.16 / -1.08 / -1.15 ms -- a net gain up to k = 16, none at 32."""
+    mode = os.environ.get("MAXK_EDGE_SEL", "auto")
+    if k % 4 or mode == "0":
+        return False
+    return mode == "1" or k <= EDGE_SEL_KMAX
+
+
+def use_edge_selectors(indptr: torch.Tensor, indices: torch.Tensor, k: int, num_cols: int,
+                       dim: Optional[int] = None) -> bool:
+    """Whether a forward should write the per-edge selector stream for its backward
+    (spgemm_forward(edge_sel_out=) -> sspmm_backward(edge_sel=)): the backward resolves to
+    "csc" (large sparse graphs without locality, where phase 1 otherwise gathers a 128-B line of
+    the selector table per edge) and edge_selectors_wanted(k).  The stream holds num_e * k
+    bytes until the backward."""
+    if indices.numel() == 0 or not edge_selectors_wanted(k):
+        return False
+    return _bwd_mode(None, k, indices.numel(), num_cols, indptr.numel() - 1, dim,
+                     (indptr, indices)) == "csc"
+
+
+def edge_selectors(indices: torch.Tensor, cbsr_idx: torch.Tensor,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 [E, k]: edge e's destination selectors, cbsr_idx[indices[e]] (k % 4 == 0), for
+    sspmm_backward(..., edge_sel=) (maxk_edge_selectors)."""
+    _need(indices, "indices", torch.int32)
+    _need(cbsr_idx, "sparse_selector", torch.uint8)
+    E, k = indices.numel(), cbsr_idx.shape[1]
+    if out is None:
+        out = torch.empty(E, k, dtype=torch.uint8, device=indices.device)
+    with torch.cuda.device(indices.device):
+        _capi.check(_lib().maxk_edge_selectors(_ptr(indices), _ptr(cbsr_idx), E, k, _ptr(out),
+                                               _stream(indices.device)), "maxk_edge_selectors")
     return out
 
 

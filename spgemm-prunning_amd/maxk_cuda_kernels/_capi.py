@@ -33,6 +33,8 @@ SIGNATURES = {
     "maxk_spgemm_forward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_spgemm_forward": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),
+    "maxk_spgemm_forward_sel": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
+                                           _i32, _i32, _i32, _p, _sz, _p, _p]),
     "maxk_spgemm_forward_accumulate": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),
     "maxk_sspmm_backward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
@@ -41,6 +43,9 @@ SIGNATURES = {
     "maxk_sspmm_backward_csc_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward_csc": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64,
                                                _i64, _i32, _i32, _i32, _p, _sz, _p]),
+    "maxk_sspmm_backward_csc_sel": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64,
+                                               _i64, _i32, _i32, _i32, _p, _sz, _p]),
+    "maxk_edge_selectors": (ctypes.c_int, [_p, _p, _i64, _i32, _p, _p]),
     "maxk_transpose_plan_workspace_size": (_sz, [_i64, _i64]),
     "maxk_transpose_plan": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _sz, _p]),
     "maxk_sspmm_backward_bucket_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),

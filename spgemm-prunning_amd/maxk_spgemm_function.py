@@ -74,6 +74,14 @@ def _f32(t):
     return t.contiguous()
 
 
+def _edge_sel_for(indptr, indices, k, num_cols, D):
+    """The [E, k] u8 buffer the forward writes each edge's selectors into when the backward
+    will be the csc form (maxk_cuda_kernels.use_edge_selectors), else None."""
+    if not maxk_cuda_kernels.use_edge_selectors(indptr, indices, k, num_cols, D):
+        return None
+    return torch.empty(indices.numel(), k, dtype=torch.uint8, device=indices.device)
+
+
 class MaxKSpGEMMFunction(Function):
     """Autograd function over the HIP forward SpGEMM / backward SSpMM (both call shapes)."""
 
@@ -105,12 +113,16 @@ class MaxKSpGEMMFunction(Function):
                 .unsqueeze(0).expand(V, -1).contiguous()
         indptr = _indptr_for(graph_indptr, warp4_metadata, num_warps, V)
         row_div = _f32(in_degrees)
+        es = _edge_sel_for(indptr, graph_indices, k, V, D)
         out = maxk_cuda_kernels.spgemm_forward(indptr, graph_indices, _f32(graph_values),
-                                               sparse_data, sparse_selector, D, row_div=row_div)
+                                               sparse_data, sparse_selector, D, row_div=row_div,
+                                               edge_sel_out=es)
         ctx.shape_v1 = (V, D)
         ctx.save_for_backward(indptr, graph_indices, graph_values, sparse_selector,
-                              row_div if row_div is not None else torch.empty(0))
+                              row_div if row_div is not None else torch.empty(0),
+                              es if es is not None else torch.empty(0))
         ctx.has_div = row_div is not None
+        ctx.has_es = es is not None
         ctx.mode = "v1"
         return out
 
@@ -126,23 +138,28 @@ class MaxKSpGEMMFunction(Function):
         D = int(dim_origin) if dim_origin is not None else FULL_DIM
         indptr = _indptr_for(graph_indptr, warp4_metadata, num_warps, V)
         row_div = _f32(degrees)
+        es = _edge_sel_for(indptr, graph_indices, k, V, D)
         out = maxk_cuda_kernels.spgemm_forward(indptr, graph_indices, _f32(graph_values), vals,
-                                               sel, D, row_div=row_div)
+                                               sel, D, row_div=row_div, edge_sel_out=es)
         ctx.save_for_backward(indptr, graph_indices, graph_values, sel,
-                              row_div if row_div is not None else torch.empty(0))
+                              row_div if row_div is not None else torch.empty(0),
+                              es if es is not None else torch.empty(0))
         ctx.has_div = row_div is not None
+        ctx.has_es = es is not None
         ctx.mode = "v4"
         return out
 
     @staticmethod
     def backward(ctx, grad_output):
-        indptr, graph_indices, graph_values, sel, row_div = ctx.saved_tensors
+        indptr, graph_indices, graph_values, sel, row_div, es = ctx.saved_tensors
         row_div = row_div if ctx.has_div else None
         g = grad_output.contiguous()
         if g.dtype != torch.float32:
             g = g.float()
-        grad_sparse = maxk_cuda_kernels.sspmm_backward(indptr, graph_indices, _f32(graph_values),
-                                                       g, sel, row_div=row_div)
+        # with the forward's edge-selector stream the backward is the csc form reading it
+        grad_sparse = maxk_cuda_kernels.sspmm_backward(
+            indptr, graph_indices, _f32(graph_values), g, sel, row_div=row_div,
+            edge_sel=es if ctx.has_es else None, mode="csc" if ctx.has_es else None)
         grads = [None] * ctx.n_inputs
         if ctx.mode == "v1":
             V, D = ctx.shape_v1

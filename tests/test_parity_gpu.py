@@ -91,6 +91,36 @@ def test_forward_accumulate_golden(mk, cuda, path, chunk):
         mk.spgemm_forward(*parts[1], *args, accumulate=True)  # needs out=
 
 
+@pytest.mark.parametrize("chunk", [0, 5, 37])
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_edge_selector_stream_golden(mk, cuda, path, chunk):
+    """maxk_spgemm_forward_sel writes edge_sel[e] = cbsr_idx[col_idx[e]] beside the unchanged
+    forward output (short rows, long rows and hub-row slabs at small chunks), and
+    maxk_sspmm_backward_csc_sel reading that stream equals the csc backward bitwise (the same
+    contributions, the same sum order) and the fixture.  (The emitting forward walks short
+    rows one at a time instead of in batches, which keeps its register use down: its output
+    matches the fixture, not the plain call bit for bit.)"""
+    z = load_golden(path)
+    rp, col, val = T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda)
+    cv, ci, D = T(z["topk_val"], cuda), T(z["topk_idx"], cuda), int(z["D"])
+    k = ci.shape[1]
+    E = col.numel()
+    div = T(z["deg"], cuda)
+    es = torch.full((E, k), 0xAB, dtype=torch.uint8, device=cuda)
+    y = mk.spgemm_forward(rp, col, val, cv, ci, D, row_div=div, chunk=chunk, edge_sel_out=es)
+    close(y, z["y_ref"])  # short rows take the one-row path here, so not bitwise the plain call
+    assert torch.equal(es, ci[col.long()])
+    if k % 4:
+        return
+    assert torch.equal(mk.edge_selectors(col, ci), es)
+    g = T(z["g"], cuda)
+    ref = mk.sspmm_backward(rp, col, val, g, ci, row_div=div, chunk=chunk, mode="csc")
+    got = mk.sspmm_backward(rp, col, val, g, ci, row_div=div, chunk=chunk, mode="csc",
+                            edge_sel=es)
+    assert torch.equal(got, ref)
+    close(got, z["grad_cbsr_ref"])
+
+
 @pytest.mark.parametrize("mode", ["auto", "pull", "bucket", "csc", "atomic"])
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
@@ -511,6 +541,19 @@ def test_forward_pack_aligned_and_not(mk, cuda, k):
     fv.copy_(T(cv, cuda))
     fi.copy_(T(ci, cuda))
     close(mk.spgemm_forward(*args, fv, fi, D, validate=False), ref)
+    # the edge-selector stream keeps the caller's bytes (duplicates, past D) whichever pack
+    # folded them, and the csc backward reading it matches the oracle (selectors >= D read 0)
+    for cvv, civ in ((T(cv, cuda), T(ci, cuda)), (fv, fi)):
+        es = torch.zeros(col.size, k, dtype=torch.uint8, device=cuda)
+        close(mk.spgemm_forward(*args, cvv, civ, D, validate=False, edge_sel_out=es), ref)
+        assert np.array_equal(es.cpu().numpy(), ci[col])
+    if k % 4 == 0:
+        g = rng.standard_normal((V, D), dtype=np.float32)
+        g_pad = np.zeros((V, 256), np.float32)
+        g_pad[:, :D] = g
+        gs = mk.sspmm_backward(*args, T(g, cuda), T(ci, cuda), mode="csc", validate=False,
+                               edge_sel=es)
+        close(gs, O.sspmm_bwd(row_ptr, col, val, g_pad, ci))
 
 
 def test_selectors_past_D_read_zero(mk, cuda):
