@@ -146,3 +146,31 @@ def test_full_size_topk_gaussian(cuda, k):
     tail = x[2_097_152:]
     cv, ci = mk.topk_cbsr(tail, k)
     check_topk_rows(tail, cv, ci, k, f"gaussian tail k={k}")
+
+
+def test_full_size_edge_selector_stream(cuda):
+    """ogbn-products-sized, k = 8 (where bench and layers use it): the forward's per-edge
+    selector stream equals cbsr_idx[col_idx] on every edge, its output matches the plain
+    forward, and the csc backward reading the stream equals the table-reading one bitwise."""
+    import maxk_cuda_kernels as mk
+    rp, col, _, _ = graph("products", cuda)
+    V, E, D, k = rp.numel() - 1, col.numel(), 256, 8
+    gen = torch.Generator(device=cuda).manual_seed(77)
+    val = torch.rand(E, generator=gen, device=cuda)
+    x = torch.rand(V, D, generator=gen, device=cuda)
+    G = torch.rand(V, D, generator=gen, device=cuda)
+    cv, ci = mk.topk_cbsr(x, k)
+    del x
+    es = torch.empty(E, k, dtype=torch.uint8, device=cuda)
+    y = mk.spgemm_forward(rp, col, val, cv, ci, D, validate=False, edge_sel_out=es)
+    y0 = mk.spgemm_forward(rp, col, val, cv, ci, D, validate=False)
+    assert bool(((y - y0).abs() <= 1e-5 * y0.abs().clamp(min=1)).all())
+    del y, y0
+    for c0 in range(0, E, 1 << 25):  # the stream, in chunks
+        c1 = min(E, c0 + (1 << 25))
+        assert torch.equal(es[c0:c1], ci[col[c0:c1].long()])
+    plan = mk.transpose_plan(col, V)
+    a = mk.sspmm_backward(rp, col, val, G, ci, mode="csc", plan=plan, validate=False)
+    b = mk.sspmm_backward(rp, col, val, G, ci, mode="csc", plan=plan, validate=False,
+                          edge_sel=es)
+    assert torch.equal(a, b)
