@@ -45,6 +45,7 @@ def main():
                 continue
             d[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     per_kernel = collections.defaultdict(dict)  # base name -> counter -> mean bytes
+    n_disp = {}
     for (k, c), v in sorted(d.items()):
         m = sum(v) / len(v)
         extra = ""
@@ -53,7 +54,12 @@ def main():
         elif c == "WRITE_SIZE":
             extra = f"  -> {m * 1024 / 1e9:.3f} GB"
         if c in ("FETCH_SIZE", "WRITE_SIZE"):
-            per_kernel[base(k)][c] = per_kernel[base(k)].get(c, 0.0) + m * 1024
+            # template variants of one kernel (e.g. a validating call's plain forward beside
+            # the timed emitting one): the variant with the most dispatches stands for it
+            prev = per_kernel[base(k)].get(c)
+            if prev is None or len(v) > n_disp[(base(k), c)]:
+                per_kernel[base(k)][c] = m * 1024
+                n_disp[(base(k), c)] = len(v)
         print(f"{k[:48]:48s} {c:14s} n={len(v):3d} mean={m:.5g}{extra}")
     if a.traffic_out:
         from bench import OP_KERNELS
