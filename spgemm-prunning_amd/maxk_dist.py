@@ -180,8 +180,11 @@ class ShardedMaxK:
             self._halo_plan(cols, starts)
         self.values = values[e0:e1].to(self.device, torch.float32).contiguous()
         self._plans = {}
+        # default: pipelined at world > 1; an explicit part count also applies at world 1 (the
+        # one-GPU RCCL test runs the async collectives and part kernels that way)
         P = self.PIPELINE if pipeline is None else int(pipeline)
-        self.pipeline = max(1, min(P, self.vmax)) if mode == "gather" and world > 1 else 1
+        on = mode == "gather" and (world > 1 or pipeline is not None)
+        self.pipeline = max(1, min(P, self.vmax)) if on else 1
         if self.pipeline > 1:
             self._split_parts(owner, loc)
 

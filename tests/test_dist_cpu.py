@@ -264,7 +264,9 @@ def _run_local(world, args, D, k):
 
 @pytest.mark.gpu
 def test_sharded_hip_single_rank_rccl(cuda):
-    """ShardedMaxK over RCCL (world 1) with the HIP kernels == the direct HIP calls == oracle."""
+    """ShardedMaxK over RCCL (world 1) with the HIP kernels == the direct HIP calls == oracle;
+    then the pipelined gather mode (3 column parts, async RCCL all-gathers and reduce-scatters
+    waited on by the compute stream, the accumulating forward) on the same communicator."""
     import maxk_cuda_kernels as mk
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ["MASTER_PORT"] = str(_free_port())
@@ -278,15 +280,20 @@ def test_sharded_hip_single_rank_rccl(cuda):
         deg = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
         tv, ti = oracle.topk(x, k)
         to = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
-        shard = maxk_dist.ShardedMaxK(to(row_ptr), to(col), to(val), 0, 1, device=cuda)
-        val_l = to(tv).requires_grad_(True)
-        y = maxk_dist.sharded_maxk_spgemm(shard, val_l, to(ti), D, to(deg))
-        y.backward(to(g))
         y_ref = oracle.spgemm_fwd(row_ptr, col, val, tv, ti, D, row_div=deg)
         gs_ref = oracle.sspmm_bwd(row_ptr, col, val, g, ti, row_div=deg)
-        np.testing.assert_allclose(y.detach().cpu().numpy(), y_ref, rtol=1e-4, atol=1e-4)
-        np.testing.assert_allclose(val_l.grad.cpu().numpy(), gs_ref, rtol=1e-4, atol=1e-4)
-        y2 = mk.spgemm_forward(to(row_ptr), to(col), to(val), to(tv), to(ti), D, row_div=to(deg))
-        assert torch.equal(y.detach(), y2)
+        for pipeline in (None, 3):
+            shard = maxk_dist.ShardedMaxK(to(row_ptr), to(col), to(val), 0, 1, device=cuda,
+                                          pipeline=pipeline)
+            assert shard.pipeline == (1 if pipeline is None else 3)
+            val_l = to(tv).requires_grad_(True)
+            y = maxk_dist.sharded_maxk_spgemm(shard, val_l, to(ti), D, to(deg))
+            y.backward(to(g))
+            np.testing.assert_allclose(y.detach().cpu().numpy(), y_ref, rtol=1e-4, atol=1e-4)
+            np.testing.assert_allclose(val_l.grad.cpu().numpy(), gs_ref, rtol=1e-4, atol=1e-4)
+            if pipeline is None:
+                y2 = mk.spgemm_forward(to(row_ptr), to(col), to(val), to(tv), to(ti), D,
+                                       row_div=to(deg))
+                assert torch.equal(y.detach(), y2)
     finally:
         dist.destroy_process_group()
