@@ -192,6 +192,39 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
                      uint16_t *bucket_dst, void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Same backward, two-phase with window-sorted contribution rows ("bsort", dim_k % 4 == 0),
+ * for large sparse graphs at small k, where every contribution row phase 2 reads would
+ * otherwise cost a whole random 128-B line (ogbn-products k = 8: 32-B rows).  The CSR edges
+ * are cut into windows of W = maxk_bsort_window(dim_k) consecutive edges; phase 1 builds a
+ * window's rows in LDS (one workgroup per window) and writes them to the window's range of T
+ * ordered by destination bucket, so the bucketed phase 2 (as maxk_sspmm_backward_bucket,
+ * fp64 LDS sums) reads a bucket's rows of one window as one run.  edge_sel (optional, u8
+ * [num_e, k], 4-B aligned; as maxk_sspmm_backward_csc_sel) replaces the cbsr_idx row
+ * gathers; cbsr_idx may be NULL when it is given, col_idx when edge_sel is given.
+ * Plan (once per graph and k): maxk_bsort_plan with the shift maxk_bucket_shift(k) --
+ * bucket_ptr / bucket_dst as maxk_bucket_plan, bucket_pos[num_e] the T row of each bucket
+ * entry, win_src[num_e] (u16) the edge (relative to its window) whose row T row p holds.
+ * Replaces the same reference kernels as maxk_sspmm_backward.
+ * ------------------------------------------------------------------------- */
+int32_t maxk_bsort_window(int32_t dim_k); /* -1 unless dim_k % 4 == 0 in [4, 256] */
+size_t maxk_bsort_plan_workspace_size(int64_t num_cols, int64_t num_e);
+int maxk_bsort_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e, int32_t dim_k,
+                    int32_t bucket_shift, int32_t *bucket_ptr, int32_t *bucket_pos,
+                    uint16_t *bucket_dst, uint16_t *win_src, void *workspace,
+                    size_t workspace_bytes, void *stream);
+size_t maxk_sspmm_backward_bsort_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                int64_t num_e, int32_t dim_origin,
+                                                int32_t dim_k);
+int maxk_sspmm_backward_bsort(const int32_t *row_ptr, const int32_t *col_idx,
+                              const float *edge_val, const float *grad_out, const float *row_div,
+                              const uint8_t *cbsr_idx, const uint8_t *edge_sel,
+                              const int32_t *bucket_ptr, const int32_t *bucket_pos,
+                              const uint16_t *bucket_dst, const uint16_t *win_src,
+                              int32_t bucket_shift, float *grad_cbsr, int64_t num_rows,
+                              int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                              void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Backward, pull form (no contribution rows): the same result as maxk_sspmm_backward,
  * summed per tile (row slice x destination bucket of 2^shift columns) from G / row_div
  * gathered directly, fp64 LDS accumulation, then the slices of a bucket added in slice

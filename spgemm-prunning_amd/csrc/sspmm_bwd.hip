@@ -605,6 +605,202 @@ __global__ __launch_bounds__(kBlock) void bucket_fixup_kernel(
     *o = a;
 }
 
+// ---- window-sorted phase 1 ("bsort", maxk_sspmm_backward_bsort) ---------------------------
+// On a large sparse graph every contribution row the bucketed phase 2 (or csc) reads lies on
+// its own random line: at k = 8 a 32-B row costs a 128-B line, so phase 2 runs at the
+// fabric's random-line rate whatever k.  Here the edges are cut into windows
+// of W consecutive CSR edges (W * k * 4 B fill the LDS stage), one 1024-thread workgroup per
+// window: its waves compute the window's rows into LDS in CSR order (as phase 1 computes
+// them), then the workgroup writes them out to T[window] ordered by destination bucket
+// (win_src: T row w0 + i holds edge w0 + win_src[w0 + i]; a stable sort on the bucket, from
+// maxk_bsort_plan).  A bucket's rows of one window are then one contiguous run (ogbn-products
+// k = 8, W = 4608, 1196 buckets: ~4 rows, 128 B), read by bucket_sum_kernel through the plan's
+// positions.  The writes stay coalesced: the reorder happens in LDS.
+constexpr int kBsortThreads = 1024;
+constexpr int kBsortWaves = kBsortThreads / kWave;
+constexpr int kBsortStageFloats = (160 * 1024 - kBsortWaves * kMaxDim * 4) / 4;  // 144 KiB
+
+// Edges [sb, se) of one staged row (sb < se) into the stage (stage = the row of edge sb):
+// LR lanes per edge, 4 consecutive l per lane, U wave instructions of edges in flight, the
+// next batch's weights (and columns) loaded while this one computes.  ES: selectors from the
+// per-edge stream, else gathered from the destination's row of cbsr_idx.
+template <int LR, int U, bool ES>
+__device__ __forceinline__ void push_stage(const float *g_lds, const int32_t *__restrict__ col_idx,
+                                           const float *__restrict__ edge_val,
+                                           const uint8_t *__restrict__ cbsr_idx,
+                                           const uint8_t *__restrict__ esel, float *stage, int sb,
+                                           int se, int k, int lane) {
+    constexpr int G = kWave / LR;
+    constexpr int GU = G * U;
+    const int grp = lane / LR;
+    const int q = lane % LR;
+    const int k4 = k >> 2;
+    const int n = se - sb;
+    const auto crs = wave_buffer(col_idx + sb, (uint32_t)n * 4u);
+    const auto vrs = wave_buffer(edge_val + sb, (uint32_t)n * 4u);
+    const auto srs = ES ? wave_buffer(esel + (size_t)(uint32_t)sb * k, (uint32_t)n * k)
+                        : wave_buffer(cbsr_idx, 0xffffffffu);
+    const uint32_t qsel = 4u * (uint32_t)(q < k4 ? q : k4 - 1);
+    int c[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int o = (u * G + grp) * 4;
+        if (!ES) c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, o, 0, 0);
+        w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, o, 0, 0));
+    }
+    for (int base = 0;; base += GU) {
+        const bool has_next = base + GU < n;  // wave-uniform
+        int cn[U];
+        float wn[U];
+        if (has_next) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int o = (base + GU + u * G + grp) * 4;
+                if (!ES) cn[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, o, 0, 0);
+                wn[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, o, 0, 0));
+            }
+        }
+        uint32_t sv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            sv[u] = __builtin_amdgcn_raw_buffer_load_b32(
+                srs,
+                ES ? (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel)
+                   : (int)((uint32_t)c[u] * (uint32_t)k + qsel),
+                0, 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = base + u * G + grp;
+            const uint32_t s = sv[u];
+            float4 x;
+            x.x = w[u] * g_lds[s & 255u];
+            x.y = w[u] * g_lds[(s >> 8) & 255u];
+            x.z = w[u] * g_lds[(s >> 16) & 255u];
+            x.w = w[u] * g_lds[s >> 24];
+            if (q < k4 && e < n) *reinterpret_cast<float4 *>(stage + (size_t)e * k + 4 * q) = x;
+        }
+        if (!has_next) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ES) c[u] = cn[u];
+            w[u] = wn[u];
+        }
+    }
+}
+
+// The row holding CSR edge e (0 <= e < row_ptr[n]): the last r with row_ptr[r] <= e, by a
+// 64-ary search of the whole wave (wave-uniform result).
+__device__ __forceinline__ int wave_row_of_edge(const int32_t *__restrict__ row_ptr, int n, int e) {
+    const int lane = lane_id();
+    int lo = 0, hi = n;  // the first p with row_ptr[p] > e lies in [lo, hi]
+    while (hi - lo > 63) {
+        const int step = (hi - lo + 62) / 63;
+        int p = lo + lane * step;
+        p = p > hi ? hi : p;
+        const uint64_t m = __ballot(row_ptr[p] > e);  // lane 63 probes hi: true
+        const int f = __builtin_ctzll(m);
+        if (f == 0) {
+            hi = lo;
+        } else {
+            const int pf = lo + f * step;
+            lo = lo + (f - 1) * step + 1;
+            hi = pf > hi ? hi : pf;
+        }
+    }
+    const int p = lo + lane;
+    const int pc = p > hi ? hi : p;
+    const uint64_t m = __ballot(p <= hi && row_ptr[pc] > e) | (1ull << 63);
+    int r = lo + __builtin_ctzll(m);
+    r = r > hi ? hi : r;
+    return r - 1;
+}
+
+template <int LR, int U, bool ES>
+__global__ __launch_bounds__(kBsortThreads) void bsort_push_kernel(
+    const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
+    const float *__restrict__ edge_val, const float *__restrict__ grad,
+    const float *__restrict__ row_div, const uint8_t *__restrict__ cbsr_idx,
+    const uint8_t *__restrict__ esel, const uint16_t *__restrict__ win_src,
+    float *__restrict__ T, int num_rows, int num_e, int D, int k, int W) {
+    __shared__ __attribute__((aligned(16))) float stage[kBsortStageFloats];
+    __shared__ __attribute__((aligned(16))) float grow[kBsortWaves][kMaxDim];
+    const int wid = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int b = MAXK_P1_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int64_t w0l = (int64_t)b * W;
+    if (w0l >= num_e) return;  // whole workgroup: padding blocks of the XCD grid
+    const int w0 = (int)w0l;
+    const int w1 = num_e - w0 > W ? w0 + W : num_e;
+    const int per = (w1 - w0 + kBsortWaves - 1) / kBsortWaves;
+    const int e0 = w0 + wid * per;
+    const int e1 = e0 + per < w1 ? e0 + per : w1;
+    float *g_lds = grow[wid];
+    *reinterpret_cast<float4 *>(&g_lds[lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e0 < e1) {
+        // rows as in sspmm_bwd_kernel: row_ptr / row_div of 64 rows one per lane, the next
+        // row's G values loaded while this row's edges run
+        int q = wave_row_of_edge(row_ptr, num_rows, e0);
+        int wb = q;
+        int rpw = row_ptr[wb + lane < num_rows ? wb + lane : num_rows];
+        float dvw = row_div ? row_div[wb + lane < num_rows ? wb + lane : num_rows - 1] : 1.f;
+        auto load_g = [&](int row, float (&g)[4]) {
+            const float *gr = grad + (int64_t)(row < num_rows ? row : num_rows - 1) * D;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = lane + kWave * i;
+                g[i] = gr[j < D ? j : D - 1];
+            }
+        };
+        float gn[4];
+        load_g(q, gn);
+        for (; q < num_rows; ++q) {
+            if (q + 1 - wb >= kWave) {
+                wb = q;
+                rpw = row_ptr[wb + lane < num_rows ? wb + lane : num_rows];
+                if (row_div) dvw = row_div[wb + lane < num_rows ? wb + lane : num_rows - 1];
+            }
+            const int rb = __builtin_amdgcn_readlane(rpw, q - wb);
+            const int re = __builtin_amdgcn_readlane(rpw, q + 1 - wb);
+            if (rb >= e1) break;
+            float g[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g[i] = gn[i];
+            if (q + 1 < num_rows) load_g(q + 1, gn);
+            const int sb = rb > e0 ? rb : e0;
+            const int se = re < e1 ? re : e1;
+            if (sb >= se) continue;
+            const float div = __builtin_bit_cast(
+                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, dvw), q - wb));
+            wave_lds_fence();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = lane + kWave * i;
+                if (j < D) g_lds[j] = row_div ? g[i] / div : g[i];
+            }
+            wave_lds_fence();
+            push_stage<LR, U, ES>(g_lds, col_idx, edge_val, cbsr_idx, esel,
+                                  stage + (size_t)(sb - w0) * k, sb, se, k, lane);
+        }
+    }
+    __syncthreads();
+    // write-out in bucket order: T row w0 + i <- staged row win_src[w0 + i], 16 B per thread,
+    // non-temporal (the 1-4 GB stream would evict the lines phase 1 re-reads)
+    const int kq = k >> 2;
+    const int nrow = w1 - w0;
+    const auto trs = wave_buffer(T + (size_t)w0 * k, (uint32_t)nrow * k * 4u);
+    const float4 *st4 = reinterpret_cast<const float4 *>(stage);
+    for (int i = threadIdx.x; i < nrow * kq; i += kBsortThreads) {
+        const int p = i / kq;
+        const int qq = i - p * kq;
+        int src = win_src[w0 + p];
+        src = src < nrow ? src : nrow - 1;
+        const float4 v = st4[src * kq + qq];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), trs, i * 16, 0,
+                                               MAXK_T_AUX);
+    }
+}
+
 // ---- pull: the backward without contribution rows -------------------------------------
 // grad_cbsr[c, :] = sum over the edges (r -> c) of w * G'[r, sel[c, :]], G' = G / row_div.
 // The pull plan (maxk_pull_plan) sorts the edges into tiles: tile t = (row slice s,
@@ -1566,6 +1762,11 @@ int bucket_part(int64_t num_e) {
     return (int)(p < 16384 ? 16384 : p);
 }
 
+static int bucket_phase2(hipStream_t s, const float *T, const int32_t *bucket_ptr,
+                         const int32_t *bucket_row, const uint16_t *bucket_dst, int bucket_shift,
+                         float *grad_cbsr, void *workspace, int64_t num_cols, int64_t num_e,
+                         int k);
+
 extern "C" size_t maxk_sspmm_backward_bucket_workspace_size(int64_t num_rows, int64_t num_cols,
                                                             int64_t num_e, int32_t dim_origin,
                                                             int32_t dim_k, int32_t chunk_edges) {
@@ -1612,13 +1813,25 @@ extern "C" int maxk_sspmm_backward_bucket(const int32_t *row_ptr, const int32_t 
                                          bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS)))
             return rc;
     }
+    return bucket_phase2(s, T, bucket_ptr, bucket_eid, bucket_dst, bucket_shift, grad_cbsr,
+                         workspace, num_cols, num_e, k);
+}
+
+// Phase 2 of the bucketed forms: bucket_sum_kernel over the bucket list (entry i reads T row
+// bucket_row[i]) and the fixup of the buckets split over parts.  The slab sits after T in
+// the workspace (maxk_sspmm_backward_bucket_workspace_size).
+static int bucket_phase2(hipStream_t s, const float *T, const int32_t *bucket_ptr,
+                         const int32_t *bucket_row, const uint16_t *bucket_dst, int bucket_shift,
+                         float *grad_cbsr, void *workspace, int64_t num_cols, int64_t num_e,
+                         int k) {
     const int64_t nb = (num_cols + (1LL << bucket_shift) - 1) >> bucket_shift;
     const int part = bucket_part(num_e);
     const int64_t parts = ceil_div(num_e, part);
     float *slab = reinterpret_cast<float *>(
         reinterpret_cast<char *>(workspace) +
-        (((size_t)(num_e + 1) * dim_k * sizeof(float) + 255) & ~(size_t)255));
+        (((size_t)(num_e + 1) * k * sizeof(float) + 255) & ~(size_t)255));
     const int nc = (int)num_cols, ne = (int)num_e, nbi = (int)nb;
+    const int32_t *bucket_eid = bucket_row;
     switch (parts > 0 ? lanes_per_edge(k / 4) : 0) {
         case 0:
             break;
@@ -1646,6 +1859,83 @@ extern "C" int maxk_sspmm_backward_bucket(const int32_t *row_ptr, const int32_t 
                        dim3(kBlock), 0, s, bucket_ptr, slab, grad_cbsr, nc, k, bucket_shift, part);
     MAXK_LAUNCHED("bucket_fixup_kernel");
     return MAXK_OK;
+}
+
+extern "C" int32_t maxk_bsort_window(int32_t dim_k) {
+    if (dim_k <= 0 || dim_k % 4 != 0 || dim_k > kMaxDim) return -1;
+    const int w = kBsortStageFloats / dim_k;
+    return w > 65536 ? 65536 : w;
+}
+
+extern "C" size_t maxk_sspmm_backward_bsort_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                           int64_t num_e, int32_t dim_origin,
+                                                           int32_t dim_k) {
+    return maxk_sspmm_backward_bucket_workspace_size(num_rows, num_cols, num_e, dim_origin, dim_k,
+                                                     0);
+}
+
+extern "C" int maxk_sspmm_backward_bsort(
+    const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val, const float *grad_out,
+    const float *row_div, const uint8_t *cbsr_idx, const uint8_t *edge_sel,
+    const int32_t *bucket_ptr, const int32_t *bucket_pos, const uint16_t *bucket_dst,
+    const uint16_t *win_src, int32_t bucket_shift, float *grad_cbsr, int64_t num_rows,
+    int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k, void *workspace,
+    size_t workspace_bytes, void *stream) {
+    clear_error();
+    if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, 0)) return rc;
+    MAXK_REQUIRE(dim_k % 4 == 0, "window-sorted backward needs dim_k %% 4 == 0, got %d", dim_k);
+    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 16 &&
+                     ((int64_t)(dim_k + 1) << bucket_shift) <= kBucketAccDoubles,
+                 "bucket_shift %d too large for dim_k %d (2^shift * (k + 1) <= %d)", bucket_shift,
+                 dim_k, kBucketAccDoubles);
+    hipStream_t s = as_stream(stream);
+    if (num_cols == 0) return MAXK_OK;
+    MAXK_REQUIRE(grad_cbsr && bucket_ptr, "grad_cbsr/bucket_ptr must not be NULL");
+    MAXK_REQUIRE(num_e == 0 || (row_ptr && edge_val && grad_out && (cbsr_idx || edge_sel) &&
+                                (edge_sel || col_idx) && bucket_pos && bucket_dst && win_src),
+                 "CSR/grad/selector/plan pointers must not be NULL");
+    MAXK_REQUIRE(!edge_sel || ((uintptr_t)edge_sel & 3) == 0, "edge_sel must be 4-B aligned");
+    const size_t need = maxk_sspmm_backward_bsort_workspace_size(num_rows, num_cols, num_e,
+                                                                 dim_origin, dim_k);
+    MAXK_REQUIRE(workspace && workspace_bytes >= need,
+                 "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
+    float *T = reinterpret_cast<float *>(workspace);
+    const int k = dim_k;
+    if (num_e > 0) {
+        MAXK_REQUIRE(num_rows > 0, "edges present but num_rows == 0");
+        const int W = maxk_bsort_window(k);
+        const int64_t nwin = ceil_div(num_e, W);
+        const dim3 grid((unsigned)(MAXK_P1_XCD ? xcd_grid(nwin) : nwin));
+        const int nr = (int)num_rows, ne = (int)num_e;
+        switch (lanes_per_edge(k / 4)) {
+#define MAXK_GO(LRV, ESV)                                                                         \
+    hipLaunchKernelGGL((bsort_push_kernel<LRV, 4, ESV>), grid, dim3(kBsortThreads), 0, s, row_ptr, \
+                       col_idx, edge_val, grad_out, row_div, cbsr_idx, edge_sel, win_src, T, nr,  \
+                       ne, dim_origin, k, W)
+#define MAXK_CASE(LRV)          \
+    case LRV:                   \
+        if (edge_sel)           \
+            MAXK_GO(LRV, true); \
+        else                    \
+            MAXK_GO(LRV, false); \
+        break;
+            MAXK_CASE(1)
+            MAXK_CASE(2)
+            MAXK_CASE(4)
+            MAXK_CASE(8)
+            MAXK_CASE(16)
+            MAXK_CASE(32)
+            MAXK_CASE(64)
+#undef MAXK_CASE
+#undef MAXK_GO
+            default:
+                set_error("unsupported lane group");
+                return MAXK_ERR_INVALID;
+        }
+        MAXK_LAUNCHED("bsort_push_kernel");
+    }
+    return bucket_phase2(s, T, bucket_ptr, bucket_pos, bucket_dst, bucket_shift, grad_cbsr,
+                         workspace, num_cols, num_e, k);
 }
 
 // ---- pull backward: C entry ------------------------------------------------------------

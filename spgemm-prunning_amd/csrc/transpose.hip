@@ -173,6 +173,107 @@ extern "C" int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_
     return MAXK_OK;
 }
 
+// ---- window-sorted plan (maxk_sspmm_backward_bsort) ---------------------------------------
+// The bucket plan, with each entry's CSR edge id replaced by the T row phase 1 stores that
+// edge's contribution in, plus win_src.  Windows are W = maxk_bsort_window(k) consecutive CSR
+// edges; a stable radix sort of (window, bucket, edge id) gives every window's edges in
+// bucket order, and since windows sort in order, the sorted position p of edge e IS its T
+// row: win_src[p] = e - window_start(p), pos[e] = p, bucket_pos[i] = pos[bucket_eid[i]].
+namespace maxk {
+namespace {
+
+__global__ void bsort_key_kernel(const int32_t *__restrict__ col_idx, int64_t num_e, int W,
+                                 int nb, int shift, int32_t *__restrict__ keys,
+                                 int32_t *__restrict__ ids) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= num_e) return;
+    int b = col_idx[e] >> shift;
+    b = b < 0 ? 0 : (b >= nb ? nb - 1 : b);  // out-of-range columns stay inside their window
+    keys[e] = (int32_t)((e / W) * nb + b);
+    ids[e] = (int32_t)e;
+}
+
+__global__ void bsort_pos_kernel(const int32_t *__restrict__ perm, int64_t num_e, int W,
+                                 uint16_t *__restrict__ win_src, int32_t *__restrict__ pos) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= num_e) return;
+    const int e = perm[p];
+    win_src[p] = (uint16_t)(e - p / W * W);
+    pos[e] = (int32_t)p;
+}
+
+__global__ void bsort_map_kernel(const int32_t *__restrict__ pos, int64_t num_e,
+                                 int32_t *__restrict__ bucket_pos) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < num_e) bucket_pos[i] = pos[bucket_pos[i]];
+}
+
+size_t bsort_sort_bytes(int64_t num_e) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t *)nullptr,
+                                             (int32_t *)nullptr, (const int32_t *)nullptr,
+                                             (int32_t *)nullptr, (int)num_e, 0, 31);
+    return bytes;
+}
+
+}  // namespace
+}  // namespace maxk
+
+extern "C" size_t maxk_bsort_plan_workspace_size(int64_t num_cols, int64_t num_e) {
+    if (num_cols < 0 || num_e <= 0) return 0;
+    const size_t a = al256((size_t)num_e * 4);
+    const size_t bucket = maxk_bucket_plan_workspace_size(num_cols, num_e);
+    const size_t own = 4 * a + al256(bsort_sort_bytes(num_e));
+    return own > bucket ? own : bucket;
+}
+
+extern "C" int maxk_bsort_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
+                               int32_t dim_k, int32_t bucket_shift, int32_t *bucket_ptr,
+                               int32_t *bucket_pos, uint16_t *bucket_dst, uint16_t *win_src,
+                               void *workspace, size_t workspace_bytes, void *stream) {
+    clear_error();
+    const int W = maxk_bsort_window(dim_k);
+    MAXK_REQUIRE(W > 0, "window-sorted plan needs dim_k %% 4 == 0 in [4, 256], got %d", dim_k);
+    MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
+    MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
+    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 16, "bucket_shift must be in [0,16]");
+    const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
+    const int64_t nwin = ceil_div(num_e, W);
+    MAXK_REQUIRE(nwin * (nb > 0 ? nb : 1) < (1LL << 31),
+                 "%lld windows x %lld buckets exceed the 31-bit sort key", (long long)nwin,
+                 (long long)nb);
+    // the bucket plan, its edge ids landing in bucket_pos (num_e == 0: bucket_ptr zeroed)
+    if (int rc = maxk_bucket_plan(col_idx, num_cols, num_e, bucket_shift, bucket_ptr, bucket_pos,
+                                  bucket_dst, workspace, workspace_bytes, stream))
+        return rc;
+    if (num_e == 0) return MAXK_OK;
+    MAXK_REQUIRE(win_src != nullptr, "win_src must not be NULL");
+    const size_t need = maxk_bsort_plan_workspace_size(num_cols, num_e);
+    MAXK_REQUIRE(workspace && workspace_bytes >= need, "workspace too small: need %zu", need);
+    hipStream_t s = as_stream(stream);
+    char *ws = reinterpret_cast<char *>(workspace);
+    const size_t a = al256((size_t)num_e * 4);
+    int32_t *keys = reinterpret_cast<int32_t *>(ws);
+    int32_t *ids = reinterpret_cast<int32_t *>(ws + a);
+    int32_t *keys_out = reinterpret_cast<int32_t *>(ws + 2 * a);
+    int32_t *perm = reinterpret_cast<int32_t *>(ws + 3 * a);
+    void *tmp = ws + 4 * a;
+    size_t tmp_bytes = workspace_bytes - 4 * a;
+    const dim3 g((unsigned)ceil_div(num_e, kBlock));
+    const int nbi = (int)(nb > 0 ? nb : 1);
+    hipLaunchKernelGGL(bsort_key_kernel, g, dim3(kBlock), 0, s, col_idx, num_e, W, nbi,
+                       (int)bucket_shift, keys, ids);
+    MAXK_LAUNCHED("bsort_key_kernel");
+    MAXK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_out, ids, perm,
+                                                (int)num_e, 0, key_bits(nwin * nbi), s));
+    int32_t *pos = keys;  // the keys are consumed by the sort
+    hipLaunchKernelGGL(bsort_pos_kernel, g, dim3(kBlock), 0, s, perm, num_e, W, win_src, pos);
+    MAXK_LAUNCHED("bsort_pos_kernel");
+    hipLaunchKernelGGL(bsort_map_kernel, g, dim3(kBlock), 0, s, pos, num_e, bucket_pos);
+    MAXK_LAUNCHED("bsort_map_kernel");
+    return MAXK_OK;
+}
+
 // ---- pull plan (the tiled pull backward, maxk_sspmm_backward_pull) -----------------------
 // Tiles t = s * n_buckets + j: rows cut into `slices` equal slices s, columns into buckets j
 // of 2^shift.  A stable radix sort of (t, edge id) lists every tile's edges in CSR order;

@@ -40,7 +40,7 @@ __all__ = [
     "topk_cbsr", "cbsr_scatter_dense", "topk_cbsr_dense", "topk_backward",
     "build_warp4_metadata", "warp4_to_indptr",
     "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
-    "transpose_plan", "bucket_plan", "pull_plan", "backward_plan", "BWD_MODES",
+    "transpose_plan", "bucket_plan", "bsort_plan", "pull_plan", "backward_plan", "BWD_MODES",
 ]
 
 FULL_DIM = 256  # the reference binding's fixed output width (cuda_kernel_bindings.cpp:70)
@@ -328,6 +328,48 @@ def bucket_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True
     return plan
 
 
+_BSORT_CACHE: "dict" = {}
+
+
+def bsort_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True):
+    """(bucket_ptr int32 [nb+1], bucket_pos int32 [E], bucket_dst uint16 [E], win_src uint16
+    [E], shift) of the CSR column indices for the window-sorted backward at width k
+    (maxk_bsort_plan): the bucket plan of maxk_bucket_shift(k) with each entry's T row in
+    place of its edge id, and per T row the edge (within its window of maxk_bsort_window(k)
+    CSR edges) phase 1 stores there.  Built once per graph and k on the GPU; cached per
+    `indices` tensor object (and its version counter)."""
+    _need(indices, "indices", torch.int32)
+    L = _lib()
+    if int(L.maxk_bsort_window(int(k))) <= 0:
+        raise RuntimeError(f"bsort_plan: k must be a multiple of 4 in [4, 256], got {k}")
+    shift = int(L.maxk_bucket_shift(int(k)))
+    key = (id(indices), int(k))
+    hit = _BSORT_CACHE.get(key)
+    if cache and hit is not None:
+        ref, nc, ver, plan = hit
+        if ref() is indices and nc == num_cols and ver == indices._version:
+            return plan
+    dev = indices.device
+    E = indices.numel()
+    nb = int(L.maxk_bucket_count(num_cols, shift))
+    bptr = torch.empty(nb + 1, dtype=torch.int32, device=dev)
+    bpos = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
+    bdst = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
+    wsrc = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
+    ws = torch.empty(max(1, L.maxk_bsort_plan_workspace_size(num_cols, E)), dtype=torch.uint8,
+                     device=dev)
+    with torch.cuda.device(dev):
+        _capi.check(L.maxk_bsort_plan(_ptr(indices), num_cols, E, int(k), shift, _ptr(bptr),
+                                      _ptr(bpos), _ptr(bdst), _ptr(wsrc), _ptr(ws), ws.numel(),
+                                      _stream(dev)), "maxk_bsort_plan")
+    plan = (bptr, bpos, bdst, wsrc, shift)
+    if cache:
+        if key not in _BSORT_CACHE:
+            weakref.finalize(indices, _BSORT_CACHE.pop, key, None)
+        _BSORT_CACHE[key] = (weakref.ref(indices), int(num_cols), indices._version, plan)
+    return plan
+
+
 _PULL_CACHE: dict = {}
 
 
@@ -471,7 +513,7 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
     return plan
 
 
-BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid")
+BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid", "bsort")
 
 
 _LOCALITY: "dict" = {}
@@ -581,8 +623,8 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
             loc = pull_locality(graph[0], graph[1], int(L.maxk_pull_shift(int(k))))
             code = int(L.maxk_backward_mode_auto(rows, num_cols, num_e, D, int(k), loc))
         mode = _MODE_OF_CODE[code]
-    if mode == "bucket" and k % 4 != 0:
-        raise RuntimeError(f"backward mode 'bucket' needs k % 4 == 0, got k={k}")
+    if mode in ("bucket", "bsort") and k % 4 != 0:
+        raise RuntimeError(f"backward mode '{mode}' needs k % 4 == 0, got k={k}")
     if mode == "pull" and k % 4 != 0 and k > 64:
         raise RuntimeError(f"backward mode 'pull' needs k % 4 == 0 or k <= 64, got k={k}")
     if mode == "pull" and dim is not None and dim % 4 != 0:
@@ -609,6 +651,8 @@ def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[s
         return pull_plan(indptr, indices, values, num_cols, k, dim or 256)
     if mode == "bucket":
         return bucket_plan(indices, num_cols, k)
+    if mode == "bsort":
+        return bsort_plan(indices, num_cols, k)
     if mode == "csc":
         return transpose_plan(indices, num_cols)
     return None
@@ -622,8 +666,9 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                    edge_sel: Optional[torch.Tensor] = None) -> torch.Tensor:
     """grad_cbsr[num_cols, k] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]].
 
-    edge_sel (uint8 [E, k], k % 4 == 0; mode "csc", ignored by the others): the selectors per
-    edge (edge_selectors(), or the forward's by-product), read in CSR order instead of gathered.
+    edge_sel (uint8 [E, k], k % 4 == 0; modes "csc" and "bsort", ignored by the others): the
+    selectors per edge (edge_selectors(), or the forward's by-product), read in CSR order
+    instead of gathered.
 
     mode "auto" (default; MAXK_BWD_MODE overrides): "pull", "hybrid" or "csc", see _bwd_mode.
     mode "pull": per tile (row slice, destination bucket), the k values of every edge
@@ -636,6 +681,10 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     the graph's bucket plan (built once and cached, or `plan=` from bucket_plan()).
     mode "csc": two-phase, atomic-free and bitwise deterministic, using the graph's
     transpose plan (built once and cached, or `plan=` from transpose_plan()).
+    mode "bsort" (k % 4 == 0): two-phase like "bucket", phase 1 writing each window of
+    maxk_bsort_window(k) CSR edges' rows ordered by destination bucket (staged in LDS), so
+    phase 2 reads a bucket's rows of a window as one run -- for large sparse graphs at small
+    k, where a csc or bucket phase 2 pays a whole random line per 32-B row (bsort_plan()).
     mode "atomic": one global fp32 atomic per (edge, l); no preprocessing.
     mode "hybrid" (k % 4 == 0; "auto" picks it on sparse graphs with locality): the pull
     over the dense tiles of the pull plan, on a second stream, beside csc over the other
@@ -740,6 +789,22 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                 _ptr(cbsr_idx), _ptr(bptr), _ptr(beid), _ptr(bdst), shift, _ptr(out), num_rows,
                 num_cols, E, D, k, chunk, _ptr(ws), ws.numel(), _stream(dev)),
                 "maxk_sspmm_backward_bucket")
+        return out
+    if mode == "bsort":
+        bptr, bpos, bdst, wsrc, shift = (plan if plan is not None
+                                         else bsort_plan(indices, num_cols, k))
+        if edge_sel is not None:
+            _need(edge_sel, "edge_sel", torch.uint8)
+            if tuple(edge_sel.shape) != (E, k):
+                raise RuntimeError("edge_sel must be [num_e, k]")
+        ws_bytes = L.maxk_sspmm_backward_bsort_workspace_size(num_rows, num_cols, E, D, k)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            _capi.check(L.maxk_sspmm_backward_bsort(
+                _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
+                _ptr(cbsr_idx), _ptr(edge_sel), _ptr(bptr), _ptr(bpos), _ptr(bdst), _ptr(wsrc),
+                shift, _ptr(out), num_rows, num_cols, E, D, k, _ptr(ws), ws.numel(),
+                _stream(dev)), "maxk_sspmm_backward_bsort")
         return out
     if mode == "atomic":
         ws_bytes = L.maxk_sspmm_backward_workspace_size(num_rows, num_cols, E, D, k, chunk)

@@ -121,13 +121,13 @@ def test_edge_selector_stream_golden(mk, cuda, path, chunk):
     close(got, z["grad_cbsr_ref"])
 
 
-@pytest.mark.parametrize("mode", ["auto", "pull", "bucket", "csc", "atomic"])
+@pytest.mark.parametrize("mode", ["auto", "pull", "bucket", "bsort", "csc", "atomic"])
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_backward_golden(mk, cuda, path, chunk, mode):
     z = load_golden(path)
-    if mode == "bucket" and z["topk_idx"].shape[1] % 4:
-        pytest.skip("bucket mode needs k % 4 == 0")
+    if mode in ("bucket", "bsort") and z["topk_idx"].shape[1] % 4:
+        pytest.skip(f"{mode} mode needs k % 4 == 0")
     if mode == "pull" and int(z["D"]) % 4:
         pytest.skip("pull mode needs D % 4 == 0")
     gs = mk.sspmm_backward(T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda),
@@ -163,6 +163,63 @@ def test_bucket_plan(mk, cuda, path):
         assert np.array_equal(bptr.cpu().numpy(),
                               np.searchsorted(col[order] >> shift, np.arange(nb + 1)))
         assert np.array_equal(bdst.cpu().numpy().astype(np.int64), col[order] & ((1 << shift) - 1))
+
+
+def bsort_layout(col, k, shift, W, nb):
+    """numpy restatement of maxk_bsort_plan: windows of W CSR edges, each sorted by
+    destination bucket (stable); T row p holds edge perm[p]."""
+    e = np.arange(col.size)
+    perm = np.lexsort((e, np.clip(col >> shift, 0, nb - 1), e // W))
+    pos = np.empty(col.size, np.int64)
+    pos[perm] = e
+    return perm, pos
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_bsort_plan(mk, cuda, path):
+    """The window-sorted plan: the bucket plan with T rows in place of edge ids, and per T row
+    its edge relative to the window (checked against numpy at the real window and at a forced
+    small one through a 16-edge graph slice)."""
+    z = load_golden(path)
+    V = z["row_ptr"].size - 1
+    col = z["col_idx"].astype(np.int64)
+    for k in (4, 8, 16, 64):
+        bptr, bpos, bdst, wsrc, shift = mk.bsort_plan(T(z["col_idx"], cuda), V, k, cache=False)
+        assert shift == mk._lib().maxk_bucket_shift(k)
+        W = mk._lib().maxk_bsort_window(k)
+        assert W == min(65536, (160 * 1024 - 16 * 1024) // (4 * k))
+        nb = (V + (1 << shift) - 1) >> shift
+        perm, pos = bsort_layout(col, k, shift, W, nb)
+        order = np.argsort(col >> shift, kind="stable")
+        assert np.array_equal(bptr.cpu().numpy(),
+                              np.searchsorted(col[order] >> shift, np.arange(nb + 1)))
+        assert np.array_equal(bdst.cpu().numpy().astype(np.int64), col[order] & ((1 << shift) - 1))
+        assert np.array_equal(bpos.cpu().numpy(), pos[order])
+        assert np.array_equal(wsrc.cpu().numpy().astype(np.int64),
+                              perm - np.arange(col.size) // W * W)
+    assert mk._lib().maxk_bsort_window(6) == -1 and mk._lib().maxk_bsort_window(0) == -1
+
+
+@pytest.mark.parametrize("k", [4, 8, 16, 32])
+def test_bsort_windows_against_oracle(mk, cuda, k):
+    """Window-sorted backward on a products-like graph of many windows (hub rows cut by window
+    and wave boundaries, empty rows, a rectangular column space): equal to the oracle, and the
+    edge-selector stream form bitwise equal to the selector-table form (same rows, same
+    order)."""
+    rng = np.random.default_rng(500 + k)
+    R, C, D = 3000, 3500, 256
+    row_ptr, col = rand_graph(rng, R, 50, hubs=((5, 3400), (2999, 1200)), empty=40, cols=C)
+    val = rng.random(col.size, dtype=np.float32)
+    cv, ci = O.topk(rng.standard_normal((C, D), dtype=np.float32), k)
+    g = rng.standard_normal((R, D), dtype=np.float32)
+    div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+    assert col.size > 10 * mk._lib().maxk_bsort_window(k)
+    args = (T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda))
+    a = mk.sspmm_backward(*args, row_div=T(div, cuda), mode="bsort")
+    close(a, O.sspmm_bwd(row_ptr, col, val, g, ci, row_div=div))
+    es = mk.edge_selectors(T(col, cuda), T(ci, cuda))
+    b = mk.sspmm_backward(*args, row_div=T(div, cuda), mode="bsort", edge_sel=es)
+    assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("path", CASES, ids=IDS)
@@ -410,7 +467,7 @@ def test_all_k_against_oracle(mk, cuda, k, D):
     # from global memory (csc_sum_kernel STAGED)
     modes = [(0, "auto"), (0, "csc"), (13, "csc"), (2048, "csc"), (4096, "csc"), (13, "atomic")]
     if k % 4 == 0:
-        modes.append((13, "bucket"))
+        modes += [(13, "bucket"), (0, "bsort")]
     if D % 4 == 0 and (k % 4 == 0 or k <= 64):
         modes.append((0, "pull"))
     for chunk, mode in modes:
@@ -434,7 +491,7 @@ def test_high_degree_against_oracle(mk, cuda, k):
     cv, ci = O.topk(x, k)
     g = rng.standard_normal((V, D), dtype=np.float32)
     div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-    for mode in ("csc", "bucket", "pull") if k % 4 == 0 else ("csc", "pull"):
+    for mode in ("csc", "bucket", "bsort", "pull") if k % 4 == 0 else ("csc", "pull"):
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, 0, mode)
         close(y, yo)
         close(gs, go)
@@ -457,7 +514,7 @@ def test_empty_graph_and_empty_rows(mk, cuda):
     col = np.array([0, 5, 49], np.int32)
     val = np.array([1.0, 2.0, 3.0], np.float32)
     for chunk in (0, 1, 2, 7):
-        for mode in ("pull", "bucket", "csc", "atomic"):
+        for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
             y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=chunk,
                                      mode=mode)
             close(y, yo)
@@ -479,7 +536,7 @@ def test_zero_rows(mk, cuda):
     y = mk.spgemm_forward(row_ptr, col, val, cv, ci, D)
     assert y.shape == (0, D)
     g = torch.zeros(0, D, device=cuda)
-    for mode in ("pull", "bucket", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
         gs = torch.full((ncols, k), 7.0, device=cuda)
         mk.sspmm_backward(row_ptr, col, val, g, ci, out=gs, mode=mode)
         torch.cuda.synchronize()
@@ -498,7 +555,7 @@ def test_output_fully_overwritten(mk, cuda):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
                           D, out=out, chunk=9)
     close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, D))
-    for mode in ("pull", "bucket", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
         gout = torch.full((V, k), float("nan"), device=cuda)
         gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
                                T(ci, cuda), out=gout, mode=mode, chunk=7)
@@ -578,7 +635,7 @@ def test_selectors_past_D_read_zero(mk, cuda):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda),
                           T(ci, cuda), D, validate=False)
     close(y, yo)
-    for mode in ("pull", "bucket", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
         gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
                                T(ci, cuda), mode=mode, validate=False)
         close(gs, go)
@@ -595,7 +652,7 @@ def test_rectangular_shard(mk, cuda):
     val = rng.random(col.size, dtype=np.float32)
     cv, ci = O.topk(rng.standard_normal((C, D), dtype=np.float32), k)
     g = rng.standard_normal((R, D), dtype=np.float32)
-    for mode in ("pull", "bucket", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=64, mode=mode)
         assert y.shape == (R, D) and gs.shape == (C, k)
         close(y, yo)
@@ -732,7 +789,7 @@ def test_hipgraph_capture(mk, cuda):
     close(out, z["y_ref"])
 
 
-@pytest.mark.parametrize("mode", ["pull", "bucket", "csc", "hybrid", "atomic"])
+@pytest.mark.parametrize("mode", ["pull", "bucket", "bsort", "csc", "hybrid", "atomic"])
 def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch, mode):
     """Default (validate-once) mode: the first call may be inside a capture; forward and the
     two-phase backward (with its plan built beforehand) both replay correctly."""
