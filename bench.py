@@ -47,6 +47,7 @@ OP_KERNELS = {
     "sspmm_backward_pull": ["pull_q_kernel", "pull_reduce_kernel", "pull_sel4_kernel",
                             "pull_sel_kernel", "pull_tile_kernel", "gprime_kernel"],
     "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
+    "sspmm_backward_bsort": ["bsort_push_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
     # csc over the sparse tiles' edges, then the pull over the dense ones, accumulating
     "sspmm_backward_hybrid": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>",
@@ -296,7 +297,7 @@ def main():
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--bwd-mode", default="auto",
-                    choices=["auto", "pull", "bucket", "csc", "atomic", "hybrid"])
+                    choices=["auto", "pull", "bucket", "csc", "atomic", "hybrid", "bsort"])
     ap.add_argument("--graph-dir", default=None,
                     help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
     ap.add_argument("--no-cpu-spmm", action="store_true")
@@ -459,11 +460,11 @@ def main():
     t_plan = time.perf_counter() - t_plan
 
     pipelined = world > 1 and shard.pipeline > 1
-    # csc backward: the forward writes each edge's selectors, phase 1 reads them in order
-    # (maxk_spgemm_forward_sel / maxk_sspmm_backward_csc_sel) where that pays: k <= 16 by
-    # default, MAXK_EDGE_SEL=0/1 off / on (mk.edge_selectors_wanted)
+    # csc / bsort backward: the forward writes each edge's selectors, phase 1 reads them in
+    # order (maxk_spgemm_forward_sel / maxk_sspmm_backward_csc_sel / _bsort) where that pays:
+    # k <= 16 by default, MAXK_EDGE_SEL=0/1 off / on (mk.edge_selectors_wanted)
     es = (torch.empty(El, k, dtype=torch.uint8, device=dev)
-          if (not pipelined and args.bwd_mode == "csc" and El > 0
+          if (not pipelined and args.bwd_mode in ("csc", "bsort") and El > 0
               and mk.edge_selectors_wanted(k)) else None)
     if pipelined:  # the parts' plans (per-graph setup, untimed), in the bench's backward mode
         shard.kernels.bwd_mode = args.bwd_mode

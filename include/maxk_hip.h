@@ -203,14 +203,16 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
  * gathers; cbsr_idx may be NULL when it is given, col_idx when edge_sel is given.
  * Plan (once per graph and k): maxk_bsort_plan with the shift maxk_bucket_shift(k) --
  * bucket_ptr / bucket_dst as maxk_bucket_plan, bucket_pos[num_e] the T row of each bucket
- * entry, win_src[num_e] (u16) the edge (relative to its window) whose row T row p holds.
+ * entry, win_src[num_e] (u16) the edge (relative to its window) whose row T row p holds,
+ * edge_row[num_e] the source row of every CSR edge.
  * Replaces the same reference kernels as maxk_sspmm_backward.
  * ------------------------------------------------------------------------- */
 int32_t maxk_bsort_window(int32_t dim_k); /* -1 unless dim_k % 4 == 0 in [4, 256] */
 size_t maxk_bsort_plan_workspace_size(int64_t num_cols, int64_t num_e);
-int maxk_bsort_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e, int32_t dim_k,
-                    int32_t bucket_shift, int32_t *bucket_ptr, int32_t *bucket_pos,
-                    uint16_t *bucket_dst, uint16_t *win_src, void *workspace,
+int maxk_bsort_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t num_rows,
+                    int64_t num_cols, int64_t num_e, int32_t dim_k, int32_t bucket_shift,
+                    int32_t *bucket_ptr, int32_t *bucket_pos, uint16_t *bucket_dst,
+                    uint16_t *win_src, int32_t *edge_row, void *workspace,
                     size_t workspace_bytes, void *stream);
 size_t maxk_sspmm_backward_bsort_workspace_size(int64_t num_rows, int64_t num_cols,
                                                 int64_t num_e, int32_t dim_origin,
@@ -220,7 +222,8 @@ int maxk_sspmm_backward_bsort(const int32_t *row_ptr, const int32_t *col_idx,
                               const uint8_t *cbsr_idx, const uint8_t *edge_sel,
                               const int32_t *bucket_ptr, const int32_t *bucket_pos,
                               const uint16_t *bucket_dst, const uint16_t *win_src,
-                              int32_t bucket_shift, float *grad_cbsr, int64_t num_rows,
+                              const int32_t *edge_row, int32_t bucket_shift, float *grad_cbsr,
+                              int64_t num_rows,
                               int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
                               void *workspace, size_t workspace_bytes, void *stream);
 
@@ -310,7 +313,10 @@ int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *
  *   least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(dim_k) columns) or a G of at
  *   most 64 MiB; else MAXK_BWD_BUCKET on such a dense graph at dim_k <= 16; else MAXK_BWD_HYBRID
  *   when pull_locality (maxk_pull_locality at maxk_pull_shift(dim_k); < 0 = unknown) reaches
- *   MAXK_HYBRID_LOCALITY and dim_k % 4 == 0; else MAXK_BWD_CSC.
+ *   MAXK_HYBRID_LOCALITY and dim_k % 4 == 0; else MAXK_BWD_BSORT at dim_k % 4 == 0,
+ *   dim_k <= MAXK_BSORT_KMAX when a window of maxk_bsort_window(dim_k) edges holds at least 2
+ *   rows per destination bucket on average (W * 2^maxk_bucket_shift(dim_k) >= 2 * num_cols;
+ *   ogbn-products k = 8: 4.3); else MAXK_BWD_CSC.  Only csc is bitwise repeatable.
  * maxk_pull_locality (synchronous): num_e / occupied (source row, bucket of 2^bucket_shift
  *   columns) pairs, columns sorted within rows; workspace >= 8 bytes.
  * maxk_hybrid_plan (synchronous): from the graph's pull plan (maxk_pull_plan with bucket_shift,
@@ -334,6 +340,8 @@ int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *
 #define MAXK_BWD_BUCKET 2
 #define MAXK_BWD_HYBRID 3
 #define MAXK_BWD_ATOMIC 4
+#define MAXK_BWD_BSORT 5
+#define MAXK_BSORT_KMAX 8
 #define MAXK_HYBRID_LOCALITY 1.5
 #define MAXK_HYBRID_DENSITY 0.5f
 #define MAXK_HYBRID_PRESCALED 1

@@ -162,6 +162,9 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_TOPK_FENCE_WAIT  // tools only: s_waitcnt lgkmcnt(0) in the four-row top-k's fences
 #define MAXK_TOPK_FENCE_WAIT 0
 #endif
+#ifndef MAXK_BSORT_U  // window-sorted phase 1: wave instructions of edges per batch
+#define MAXK_BSORT_U 2
+#endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
 #endif

@@ -609,122 +609,36 @@ __global__ __launch_bounds__(kBlock) void bucket_fixup_kernel(
 // On a large sparse graph every contribution row the bucketed phase 2 (or csc) reads lies on
 // its own random line: at k = 8 a 32-B row costs a 128-B line, so phase 2 runs at the
 // fabric's random-line rate whatever k.  Here the edges are cut into windows
-// of W consecutive CSR edges (W * k * 4 B fill the LDS stage), one 1024-thread workgroup per
-// window: its waves compute the window's rows into LDS in CSR order (as phase 1 computes
-// them), then the workgroup writes them out to T[window] ordered by destination bucket
-// (win_src: T row w0 + i holds edge w0 + win_src[w0 + i]; a stable sort on the bucket, from
-// maxk_bsort_plan).  A bucket's rows of one window are then one contiguous run (ogbn-products
-// k = 8, W = 4608, 1196 buckets: ~4 rows, 128 B), read by bucket_sum_kernel through the plan's
-// positions.  The writes stay coalesced: the reorder happens in LDS.
+// of W consecutive CSR edges (W * k * 4 B fill the 160 KiB LDS stage), one 1024-thread
+// workgroup per window: its waves compute the window's rows into LDS in CSR order, then the
+// workgroup writes them out to T[window] ordered by destination bucket (win_src: T row
+// w0 + i holds edge w0 + win_src[w0 + i]; a stable sort on the bucket, from maxk_bsort_plan).
+// A bucket's rows of one window are then one contiguous run (ogbn-products k = 8, W = 5120,
+// 1196 buckets: ~4 rows, 137 B), read by bucket_sum_kernel through the plan's positions.  The
+// writes stay coalesced: the reorder happens in LDS.
+// One workgroup per CU (the stage fills the LDS), so every wave must keep its loads in flight
+// across its share of the window: the share is walked in flat batches of edges whatever rows
+// they belong to (the source row of each edge from the plan's edge_row), each edge's k values
+// gathered straight from G (its rows sit in L2: a window spans ~100 rows on ogbn-products), and
+// batch i + 2's weights / selectors / rows and batch i + 1's gathers are issued before batch i
+// is computed.  Per-row G staging in LDS as in sspmm_bwd_kernel cost one exposed load latency
+// per row segment at this occupancy (2.68 vs 1.45 ms for the CSR-order phase 1, products k=8).
 constexpr int kBsortThreads = 1024;
 constexpr int kBsortWaves = kBsortThreads / kWave;
-constexpr int kBsortStageFloats = (160 * 1024 - kBsortWaves * kMaxDim * 4) / 4;  // 144 KiB
-
-// Edges [sb, se) of one staged row (sb < se) into the stage (stage = the row of edge sb):
-// LR lanes per edge, 4 consecutive l per lane, U wave instructions of edges in flight, the
-// next batch's weights (and columns) loaded while this one computes.  ES: selectors from the
-// per-edge stream, else gathered from the destination's row of cbsr_idx.
-template <int LR, int U, bool ES>
-__device__ __forceinline__ void push_stage(const float *g_lds, const int32_t *__restrict__ col_idx,
-                                           const float *__restrict__ edge_val,
-                                           const uint8_t *__restrict__ cbsr_idx,
-                                           const uint8_t *__restrict__ esel, float *stage, int sb,
-                                           int se, int k, int lane) {
-    constexpr int G = kWave / LR;
-    constexpr int GU = G * U;
-    const int grp = lane / LR;
-    const int q = lane % LR;
-    const int k4 = k >> 2;
-    const int n = se - sb;
-    const auto crs = wave_buffer(col_idx + sb, (uint32_t)n * 4u);
-    const auto vrs = wave_buffer(edge_val + sb, (uint32_t)n * 4u);
-    const auto srs = ES ? wave_buffer(esel + (size_t)(uint32_t)sb * k, (uint32_t)n * k)
-                        : wave_buffer(cbsr_idx, 0xffffffffu);
-    const uint32_t qsel = 4u * (uint32_t)(q < k4 ? q : k4 - 1);
-    int c[U];
-    float w[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const int o = (u * G + grp) * 4;
-        if (!ES) c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, o, 0, 0);
-        w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, o, 0, 0));
-    }
-    for (int base = 0;; base += GU) {
-        const bool has_next = base + GU < n;  // wave-uniform
-        int cn[U];
-        float wn[U];
-        if (has_next) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int o = (base + GU + u * G + grp) * 4;
-                if (!ES) cn[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, o, 0, 0);
-                wn[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, o, 0, 0));
-            }
-        }
-        uint32_t sv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            sv[u] = __builtin_amdgcn_raw_buffer_load_b32(
-                srs,
-                ES ? (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel)
-                   : (int)((uint32_t)c[u] * (uint32_t)k + qsel),
-                0, 0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = base + u * G + grp;
-            const uint32_t s = sv[u];
-            float4 x;
-            x.x = w[u] * g_lds[s & 255u];
-            x.y = w[u] * g_lds[(s >> 8) & 255u];
-            x.z = w[u] * g_lds[(s >> 16) & 255u];
-            x.w = w[u] * g_lds[s >> 24];
-            if (q < k4 && e < n) *reinterpret_cast<float4 *>(stage + (size_t)e * k + 4 * q) = x;
-        }
-        if (!has_next) break;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!ES) c[u] = cn[u];
-            w[u] = wn[u];
-        }
-    }
-}
-
-// The row holding CSR edge e (0 <= e < row_ptr[n]): the last r with row_ptr[r] <= e, by a
-// 64-ary search of the whole wave (wave-uniform result).
-__device__ __forceinline__ int wave_row_of_edge(const int32_t *__restrict__ row_ptr, int n, int e) {
-    const int lane = lane_id();
-    int lo = 0, hi = n;  // the first p with row_ptr[p] > e lies in [lo, hi]
-    while (hi - lo > 63) {
-        const int step = (hi - lo + 62) / 63;
-        int p = lo + lane * step;
-        p = p > hi ? hi : p;
-        const uint64_t m = __ballot(row_ptr[p] > e);  // lane 63 probes hi: true
-        const int f = __builtin_ctzll(m);
-        if (f == 0) {
-            hi = lo;
-        } else {
-            const int pf = lo + f * step;
-            lo = lo + (f - 1) * step + 1;
-            hi = pf > hi ? hi : pf;
-        }
-    }
-    const int p = lo + lane;
-    const int pc = p > hi ? hi : p;
-    const uint64_t m = __ballot(p <= hi && row_ptr[pc] > e) | (1ull << 63);
-    int r = lo + __builtin_ctzll(m);
-    r = r > hi ? hi : r;
-    return r - 1;
-}
+constexpr int kBsortStageFloats = 160 * 1024 / 4;
+constexpr int kBsortPer = kBsortStageFloats / 4 / kBsortThreads;  // 16-B stage units per thread
+static_assert(kBsortStageFloats % (4 * kBsortThreads) == 0, "whole units per thread");
 
 template <int LR, int U, bool ES>
 __global__ __launch_bounds__(kBsortThreads) void bsort_push_kernel(
-    const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
+    const int32_t *__restrict__ edge_row, const int32_t *__restrict__ col_idx,
     const float *__restrict__ edge_val, const float *__restrict__ grad,
     const float *__restrict__ row_div, const uint8_t *__restrict__ cbsr_idx,
     const uint8_t *__restrict__ esel, const uint16_t *__restrict__ win_src,
-    float *__restrict__ T, int num_rows, int num_e, int D, int k, int W) {
+    float *__restrict__ T, int num_e, int D, int k, int W) {
     __shared__ __attribute__((aligned(16))) float stage[kBsortStageFloats];
-    __shared__ __attribute__((aligned(16))) float grow[kBsortWaves][kMaxDim];
+    constexpr int G = kWave / LR;  // edges per wave instruction
+    constexpr int GU = G * U;      // edges per batch
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
     const int b = MAXK_P1_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -734,70 +648,112 @@ __global__ __launch_bounds__(kBsortThreads) void bsort_push_kernel(
     const int w1 = num_e - w0 > W ? w0 + W : num_e;
     const int per = (w1 - w0 + kBsortWaves - 1) / kBsortWaves;
     const int e0 = w0 + wid * per;
-    const int e1 = e0 + per < w1 ? e0 + per : w1;
-    float *g_lds = grow[wid];
-    *reinterpret_cast<float4 *>(&g_lds[lane * 4]) = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (e0 < e1) {
-        // rows as in sspmm_bwd_kernel: row_ptr / row_div of 64 rows one per lane, the next
-        // row's G values loaded while this row's edges run
-        int q = wave_row_of_edge(row_ptr, num_rows, e0);
-        int wb = q;
-        int rpw = row_ptr[wb + lane < num_rows ? wb + lane : num_rows];
-        float dvw = row_div ? row_div[wb + lane < num_rows ? wb + lane : num_rows - 1] : 1.f;
-        auto load_g = [&](int row, float (&g)[4]) {
-            const float *gr = grad + (int64_t)(row < num_rows ? row : num_rows - 1) * D;
+    const int n = (e0 + per < w1 ? e0 + per : w1) - e0;  // this wave's edges (may be <= 0)
+    // the write-out's source rows, loaded now so they are in by the time it runs
+    const int kq = k >> 2;
+    const int nrow = w1 - w0;
+    int src[kBsortPer];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int j = lane + kWave * i;
-                g[i] = gr[j < D ? j : D - 1];
+    for (int j = 0; j < kBsortPer; ++j) {
+        const int i = threadIdx.x + j * kBsortThreads;
+        src[j] = i < nrow * kq ? (int)win_src[w0 + i / kq] : 0;
+    }
+    if (n > 0) {
+        const int grp = lane / LR;
+        const int q = lane % LR;
+        const int k4 = k >> 2;
+        const bool active = q < k4;
+        const uint32_t qsel = 4u * (uint32_t)(active ? q : k4 - 1);
+        // past the share's end the buffer loads return 0: weight 0, row 0, selector 0
+        const auto vrs = wave_buffer(edge_val + e0, (uint32_t)n * 4u);
+        const auto rrs = wave_buffer(edge_row + e0, (uint32_t)n * 4u);
+        const auto crs = wave_buffer(col_idx + (ES ? 0 : e0), ES ? 0u : (uint32_t)n * 4u);
+        const auto srs = ES ? wave_buffer(esel + (size_t)(uint32_t)e0 * k, (uint32_t)n * k)
+                            : wave_buffer(cbsr_idx, 0xffffffffu);
+        float *st = stage + (size_t)(e0 - w0) * k + 4 * q;
+        struct Batch {  // per lane and wave instruction u: weight, source row, 4 selectors
+            float w[U];
+            int r[U];
+            uint32_t s[U];
+        };
+        struct Vals {  // the 4 gathered G values and the row's divisor
+            float v[U][4];
+            float dv[U];
+        };
+        auto load_batch = [&](int base, Batch &a) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int o = (base + u * G + grp) * 4;
+                a.w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, o, 0, 0));
+                a.r[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(rrs, o, 0, 0);
+                if (ES) {
+                    a.s[u] = __builtin_amdgcn_raw_buffer_load_b32(
+                        srs, (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel), 0, 0);
+                } else {
+                    const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(crs, o, 0, 0);
+                    a.s[u] = __builtin_amdgcn_raw_buffer_load_b32(srs, (int)(c * (uint32_t)k + qsel),
+                                                                  0, 0);
+                }
             }
         };
-        float gn[4];
-        load_g(q, gn);
-        for (; q < num_rows; ++q) {
-            if (q + 1 - wb >= kWave) {
-                wb = q;
-                rpw = row_ptr[wb + lane < num_rows ? wb + lane : num_rows];
-                if (row_div) dvw = row_div[wb + lane < num_rows ? wb + lane : num_rows - 1];
-            }
-            const int rb = __builtin_amdgcn_readlane(rpw, q - wb);
-            const int re = __builtin_amdgcn_readlane(rpw, q + 1 - wb);
-            if (rb >= e1) break;
-            float g[4];
+        auto gather = [&](const Batch &a, Vals &g) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) g[i] = gn[i];
-            if (q + 1 < num_rows) load_g(q + 1, gn);
-            const int sb = rb > e0 ? rb : e0;
-            const int se = re < e1 ? re : e1;
-            if (sb >= se) continue;
-            const float div = __builtin_bit_cast(
-                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, dvw), q - wb));
-            wave_lds_fence();
+            for (int u = 0; u < U; ++u) {
+                const float *gr = grad + (int64_t)a.r[u] * D;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int j = lane + kWave * i;
-                if (j < D) g_lds[j] = row_div ? g[i] / div : g[i];
+                for (int j = 0; j < 4; ++j) {
+                    const int c = (int)((a.s[u] >> (8 * j)) & 255u);
+                    g.v[u][j] = gr[c < D ? c : 0];
+                }
+                g.dv[u] = row_div ? row_div[a.r[u]] : 1.f;
             }
-            wave_lds_fence();
-            push_stage<LR, U, ES>(g_lds, col_idx, edge_val, cbsr_idx, esel,
-                                  stage + (size_t)(sb - w0) * k, sb, se, k, lane);
+        };
+        auto compute = [&](int base, const Batch &a, const Vals &g) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float x[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = (int)((a.s[u] >> (8 * j)) & 255u);
+                    const float gv = row_div ? g.v[u][j] / g.dv[u] : g.v[u][j];
+                    x[j] = a.w[u] * (c < D ? gv : 0.f);  // a selector >= D reads 0
+                }
+                const int e = base + u * G + grp;
+                if (active && e < n)
+                    *reinterpret_cast<float4 *>(st + (size_t)e * k) =
+                        make_float4(x[0], x[1], x[2], x[3]);
+            }
+        };
+        Batch a0, a1;
+        Vals g0;
+        load_batch(0, a0);
+        gather(a0, g0);
+        if (GU < n) load_batch(GU, a1);
+        for (int base = 0; base < n; base += GU) {
+            Batch a2;
+            Vals g1;
+            if (base + 2 * GU < n) load_batch(base + 2 * GU, a2);
+            if (base + GU < n) gather(a1, g1);
+            compute(base, a0, g0);
+            a0 = a1;
+            a1 = a2;
+            g0 = g1;
         }
     }
     __syncthreads();
     // write-out in bucket order: T row w0 + i <- staged row win_src[w0 + i], 16 B per thread,
     // non-temporal (the 1-4 GB stream would evict the lines phase 1 re-reads)
-    const int kq = k >> 2;
-    const int nrow = w1 - w0;
     const auto trs = wave_buffer(T + (size_t)w0 * k, (uint32_t)nrow * k * 4u);
     const float4 *st4 = reinterpret_cast<const float4 *>(stage);
-    for (int i = threadIdx.x; i < nrow * kq; i += kBsortThreads) {
+#pragma unroll
+    for (int j = 0; j < kBsortPer; ++j) {
+        const int i = threadIdx.x + j * kBsortThreads;
         const int p = i / kq;
-        const int qq = i - p * kq;
-        int src = win_src[w0 + p];
-        src = src < nrow ? src : nrow - 1;
-        const float4 v = st4[src * kq + qq];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), trs, i * 16, 0,
-                                               MAXK_T_AUX);
+        const int sr = src[j] < nrow ? src[j] : nrow - 1;
+        const float4 v = st4[sr * kq + (i - p * kq)];
+        if (i < nrow * kq)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), trs, i * 16, 0,
+                                                   MAXK_T_AUX);
     }
 }
 
@@ -1878,7 +1834,8 @@ extern "C" int maxk_sspmm_backward_bsort(
     const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val, const float *grad_out,
     const float *row_div, const uint8_t *cbsr_idx, const uint8_t *edge_sel,
     const int32_t *bucket_ptr, const int32_t *bucket_pos, const uint16_t *bucket_dst,
-    const uint16_t *win_src, int32_t bucket_shift, float *grad_cbsr, int64_t num_rows,
+    const uint16_t *win_src, const int32_t *edge_row, int32_t bucket_shift, float *grad_cbsr,
+    int64_t num_rows,
     int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k, void *workspace,
     size_t workspace_bytes, void *stream) {
     clear_error();
@@ -1892,7 +1849,8 @@ extern "C" int maxk_sspmm_backward_bsort(
     if (num_cols == 0) return MAXK_OK;
     MAXK_REQUIRE(grad_cbsr && bucket_ptr, "grad_cbsr/bucket_ptr must not be NULL");
     MAXK_REQUIRE(num_e == 0 || (row_ptr && edge_val && grad_out && (cbsr_idx || edge_sel) &&
-                                (edge_sel || col_idx) && bucket_pos && bucket_dst && win_src),
+                                (edge_sel || col_idx) && bucket_pos && bucket_dst && win_src &&
+                                edge_row),
                  "CSR/grad/selector/plan pointers must not be NULL");
     MAXK_REQUIRE(!edge_sel || ((uintptr_t)edge_sel & 3) == 0, "edge_sel must be 4-B aligned");
     const size_t need = maxk_sspmm_backward_bsort_workspace_size(num_rows, num_cols, num_e,
@@ -1906,12 +1864,12 @@ extern "C" int maxk_sspmm_backward_bsort(
         const int W = maxk_bsort_window(k);
         const int64_t nwin = ceil_div(num_e, W);
         const dim3 grid((unsigned)(MAXK_P1_XCD ? xcd_grid(nwin) : nwin));
-        const int nr = (int)num_rows, ne = (int)num_e;
+        const int ne = (int)num_e;
         switch (lanes_per_edge(k / 4)) {
 #define MAXK_GO(LRV, ESV)                                                                         \
-    hipLaunchKernelGGL((bsort_push_kernel<LRV, 4, ESV>), grid, dim3(kBsortThreads), 0, s, row_ptr, \
-                       col_idx, edge_val, grad_out, row_div, cbsr_idx, edge_sel, win_src, T, nr,  \
-                       ne, dim_origin, k, W)
+    hipLaunchKernelGGL((bsort_push_kernel<LRV, MAXK_BSORT_U, ESV>), grid, dim3(kBsortThreads), 0, \
+                       s, edge_row, col_idx, edge_val, grad_out, row_div, cbsr_idx, edge_sel,    \
+                       win_src, T, ne, dim_origin, k, W)
 #define MAXK_CASE(LRV)          \
     case LRV:                   \
         if (edge_sel)           \

@@ -208,6 +208,19 @@ __global__ void bsort_map_kernel(const int32_t *__restrict__ pos, int64_t num_e,
     if (i < num_e) bucket_pos[i] = pos[bucket_pos[i]];
 }
 
+// Source row of every CSR edge (the COO row array): the last r with row_ptr[r] <= e.
+__global__ void bsort_rows_kernel(const int32_t *__restrict__ row_ptr, int num_rows,
+                                  int64_t num_e, int32_t *__restrict__ edge_row) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= num_e) return;
+    int lo = 0, hi = num_rows - 1;
+    while (lo < hi) {
+        const int mid = (int)(((int64_t)lo + hi + 1) >> 1);
+        if (row_ptr[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    edge_row[e] = lo;
+}
+
 size_t bsort_sort_bytes(int64_t num_e) {
     size_t bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t *)nullptr,
@@ -227,13 +240,15 @@ extern "C" size_t maxk_bsort_plan_workspace_size(int64_t num_cols, int64_t num_e
     return own > bucket ? own : bucket;
 }
 
-extern "C" int maxk_bsort_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
-                               int32_t dim_k, int32_t bucket_shift, int32_t *bucket_ptr,
-                               int32_t *bucket_pos, uint16_t *bucket_dst, uint16_t *win_src,
+extern "C" int maxk_bsort_plan(const int32_t *row_ptr, const int32_t *col_idx, int64_t num_rows,
+                               int64_t num_cols, int64_t num_e, int32_t dim_k,
+                               int32_t bucket_shift, int32_t *bucket_ptr, int32_t *bucket_pos,
+                               uint16_t *bucket_dst, uint16_t *win_src, int32_t *edge_row,
                                void *workspace, size_t workspace_bytes, void *stream) {
     clear_error();
     const int W = maxk_bsort_window(dim_k);
     MAXK_REQUIRE(W > 0, "window-sorted plan needs dim_k %% 4 == 0 in [4, 256], got %d", dim_k);
+    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
     MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
     MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
     MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 16, "bucket_shift must be in [0,16]");
@@ -247,7 +262,8 @@ extern "C" int maxk_bsort_plan(const int32_t *col_idx, int64_t num_cols, int64_t
                                   bucket_dst, workspace, workspace_bytes, stream))
         return rc;
     if (num_e == 0) return MAXK_OK;
-    MAXK_REQUIRE(win_src != nullptr, "win_src must not be NULL");
+    MAXK_REQUIRE(row_ptr && win_src && edge_row, "row_ptr/win_src/edge_row must not be NULL");
+    MAXK_REQUIRE(num_rows > 0, "edges present but num_rows == 0");
     const size_t need = maxk_bsort_plan_workspace_size(num_cols, num_e);
     MAXK_REQUIRE(workspace && workspace_bytes >= need, "workspace too small: need %zu", need);
     hipStream_t s = as_stream(stream);
@@ -271,6 +287,9 @@ extern "C" int maxk_bsort_plan(const int32_t *col_idx, int64_t num_cols, int64_t
     MAXK_LAUNCHED("bsort_pos_kernel");
     hipLaunchKernelGGL(bsort_map_kernel, g, dim3(kBlock), 0, s, pos, num_e, bucket_pos);
     MAXK_LAUNCHED("bsort_map_kernel");
+    hipLaunchKernelGGL(bsort_rows_kernel, g, dim3(kBlock), 0, s, row_ptr, (int)num_rows, num_e,
+                       edge_row);
+    MAXK_LAUNCHED("bsort_rows_kernel");
     return MAXK_OK;
 }
 

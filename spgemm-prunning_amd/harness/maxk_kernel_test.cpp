@@ -156,6 +156,7 @@ const char *mode_name(int m) {
         case MAXK_BWD_BUCKET: return "bucket";
         case MAXK_BWD_HYBRID: return "hybrid";
         case MAXK_BWD_ATOMIC: return "atomic";
+        case MAXK_BWD_BSORT: return "bsort";
     }
     return "?";
 }
@@ -166,6 +167,7 @@ int mode_of(const std::string &s) {
     if (s == "bucket") return MAXK_BWD_BUCKET;
     if (s == "hybrid") return MAXK_BWD_HYBRID;
     if (s == "atomic") return MAXK_BWD_ATOMIC;
+    if (s == "bsort") return MAXK_BWD_BSORT;
     return -1;
 }
 
@@ -173,7 +175,7 @@ int mode_of(const std::string &s) {
 // that launches it through the C ABI on the default stream.
 struct Backward {
     int mode = MAXK_BWD_CSC;
-    Buf plan_a, plan_b, plan_c, ws;
+    Buf plan_a, plan_b, plan_c, plan_d, plan_e, ws;
     // hybrid
     Buf tile_list, tile_ent, bucket_ptr, bucket_tiles, ent_pull, off_ip, off_col, off_val,
         off_cp, off_eid;
@@ -272,6 +274,29 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
                                                       b.plan_a.as<int32_t>(), b.plan_b.as<int32_t>(),
                                                       b.plan_c.as<uint16_t>(), b.shift, out, V, V,
                                                       E, D, k, 0, b.ws.p, b.ws.n, nullptr));
+            };
+            return;
+        }
+        case MAXK_BWD_BSORT: {  // window-sorted two-phase, selectors gathered from the table
+            b.shift = maxk_bucket_shift(k);
+            const int64_t nb = maxk_bucket_count(V, b.shift);
+            b.plan_a.alloc((size_t)(nb + 1) * 4);
+            b.plan_b.alloc((size_t)E * 4);
+            b.plan_c.alloc((size_t)E * 2);
+            b.plan_d.alloc((size_t)E * 2);
+            b.plan_e.alloc((size_t)E * 4);
+            Buf pws(maxk_bsort_plan_workspace_size(V, E));
+            MAXK_CHECK(maxk_bsort_plan(rp, ci, V, V, E, k, b.shift, b.plan_a.as<int32_t>(),
+                                       b.plan_b.as<int32_t>(), b.plan_c.as<uint16_t>(),
+                                       b.plan_d.as<uint16_t>(), b.plan_e.as<int32_t>(), pws.p,
+                                       pws.n, nullptr));
+            HIP_CHECK(hipDeviceSynchronize());
+            b.ws.alloc(maxk_sspmm_backward_bsort_workspace_size(V, V, E, D, k));
+            b.run = [&b, rp, ci, ev, G, row_div, S, out, V, E, D, k] {
+                MAXK_CHECK(maxk_sspmm_backward_bsort(
+                    rp, ci, ev, G, row_div, S, nullptr, b.plan_a.as<int32_t>(),
+                    b.plan_b.as<int32_t>(), b.plan_c.as<uint16_t>(), b.plan_d.as<uint16_t>(),
+                    b.plan_e.as<int32_t>(), b.shift, out, V, V, E, D, k, b.ws.p, b.ws.n, nullptr));
             };
             return;
         }
@@ -443,7 +468,7 @@ int test_graph(const Options &o, const std::string &graph, int cur, int total) {
         b.mode = mode_of(o.bwd);
         if (b.mode < 0) {  // "auto": the C ABI's rule, with the graph's locality when it matters
             b.mode = maxk_backward_mode_auto(V, V, E, D, k, -1.0);
-            if (b.mode == MAXK_BWD_CSC && k % 4 == 0 && E > 0) {
+            if ((b.mode == MAXK_BWD_CSC || b.mode == MAXK_BWD_BSORT) && k % 4 == 0 && E > 0) {
                 if (locality < 0) {
                     Buf lws(8);
                     MAXK_CHECK(maxk_pull_locality(ip.as<int32_t>(), ix.as<int32_t>(), V, E,
@@ -501,7 +526,7 @@ int main(int argc, char **argv) {
         else if (a == "--lib-runs") o.lib_runs = std::atoi(next().c_str());
         else if (a == "-h" || a == "--help") {
             std::printf("usage: %s [graph] [--dir DIR] [--k 16,32,64] [--dim 256] "
-                        "[--bwd auto|pull|csc|hybrid|bucket|atomic] [--check] [--runs 4] "
+                        "[--bwd auto|pull|csc|hybrid|bucket|bsort|atomic] [--check] [--runs 4] "
                         "[--inputs DIR] [--dump DIR]\n", argv[0]);
             return 0;
         } else if (!a.empty() && a[0] != '-') o.graph = a;
@@ -511,7 +536,7 @@ int main(int argc, char **argv) {
         }
     }
     if (o.bwd != "auto" && mode_of(o.bwd) < 0) {
-        std::fprintf(stderr, "--bwd must be auto, pull, csc, hybrid, bucket or atomic\n");
+        std::fprintf(stderr, "--bwd must be auto, pull, csc, hybrid, bucket, bsort or atomic\n");
         return 1;
     }
     if (maxk_device_count() < 1) {

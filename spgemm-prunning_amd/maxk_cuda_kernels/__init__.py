@@ -40,7 +40,7 @@ __all__ = [
     "topk_cbsr", "cbsr_scatter_dense", "topk_cbsr_dense", "topk_backward",
     "build_warp4_metadata", "warp4_to_indptr",
     "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
-    "transpose_plan", "bucket_plan", "bsort_plan", "pull_plan", "backward_plan", "BWD_MODES",
+    "transpose_plan", "bucket_plan", "bsort_plan", "pull_plan", "edge_selector_mode", "backward_plan", "BWD_MODES",
 ]
 
 FULL_DIM = 256  # the reference binding's fixed output width (cuda_kernel_bindings.cpp:70)
@@ -331,42 +331,50 @@ def bucket_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True
 _BSORT_CACHE: "dict" = {}
 
 
-def bsort_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True):
+def bsort_plan(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int, k: int,
+               cache: bool = True):
     """(bucket_ptr int32 [nb+1], bucket_pos int32 [E], bucket_dst uint16 [E], win_src uint16
-    [E], shift) of the CSR column indices for the window-sorted backward at width k
+    [E], edge_row int32 [E], shift) of a CSR graph for the window-sorted backward at width k
     (maxk_bsort_plan): the bucket plan of maxk_bucket_shift(k) with each entry's T row in
-    place of its edge id, and per T row the edge (within its window of maxk_bsort_window(k)
-    CSR edges) phase 1 stores there.  Built once per graph and k on the GPU; cached per
-    `indices` tensor object (and its version counter)."""
+    place of its edge id, per T row the edge (within its window of maxk_bsort_window(k) CSR
+    edges) phase 1 stores there, and the source row of every edge.  Built once per graph and k on the GPU; cached per
+    (indptr, indices) tensor objects (and their version counters)."""
+    _need(indptr, "indptr", torch.int32)
     _need(indices, "indices", torch.int32)
     L = _lib()
     if int(L.maxk_bsort_window(int(k))) <= 0:
         raise RuntimeError(f"bsort_plan: k must be a multiple of 4 in [4, 256], got {k}")
     shift = int(L.maxk_bucket_shift(int(k)))
-    key = (id(indices), int(k))
+    key = (id(indptr), id(indices), int(k))
     hit = _BSORT_CACHE.get(key)
     if cache and hit is not None:
-        ref, nc, ver, plan = hit
-        if ref() is indices and nc == num_cols and ver == indices._version:
+        rp, ri, nc, pv, vi, plan = hit
+        if (rp() is indptr and ri() is indices and nc == num_cols and pv == indptr._version
+                and vi == indices._version):
             return plan
     dev = indices.device
     E = indices.numel()
+    num_rows = indptr.numel() - 1
     nb = int(L.maxk_bucket_count(num_cols, shift))
     bptr = torch.empty(nb + 1, dtype=torch.int32, device=dev)
     bpos = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
     bdst = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
     wsrc = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
+    wrow = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
     ws = torch.empty(max(1, L.maxk_bsort_plan_workspace_size(num_cols, E)), dtype=torch.uint8,
                      device=dev)
     with torch.cuda.device(dev):
-        _capi.check(L.maxk_bsort_plan(_ptr(indices), num_cols, E, int(k), shift, _ptr(bptr),
-                                      _ptr(bpos), _ptr(bdst), _ptr(wsrc), _ptr(ws), ws.numel(),
-                                      _stream(dev)), "maxk_bsort_plan")
-    plan = (bptr, bpos, bdst, wsrc, shift)
+        _capi.check(L.maxk_bsort_plan(_ptr(indptr), _ptr(indices), num_rows, num_cols, E, int(k),
+                                      shift, _ptr(bptr), _ptr(bpos), _ptr(bdst), _ptr(wsrc),
+                                      _ptr(wrow), _ptr(ws), ws.numel(), _stream(dev)),
+                    "maxk_bsort_plan")
+    plan = (bptr, bpos, bdst, wsrc, wrow, shift)
     if cache:
         if key not in _BSORT_CACHE:
-            weakref.finalize(indices, _BSORT_CACHE.pop, key, None)
-        _BSORT_CACHE[key] = (weakref.ref(indices), int(num_cols), indices._version, plan)
+            for t in (indptr, indices):
+                weakref.finalize(t, _BSORT_CACHE.pop, key, None)
+        _BSORT_CACHE[key] = (weakref.ref(indptr), weakref.ref(indices), int(num_cols),
+                             indptr._version, indices._version, plan)
     return plan
 
 
@@ -429,7 +437,7 @@ _HYBRID_CACHE: "dict" = {}
 MAXK_PULL_NO_REDUCE, MAXK_PULL_REDUCE_ONLY = 2, 4  # include/maxk_hip.h
 MAXK_HYBRID_PRESCALED = 1
 # maxk_backward_mode_auto's codes (include/maxk_hip.h MAXK_BWD_*)
-_MODE_OF_CODE = {0: "pull", 1: "csc", 2: "bucket", 3: "hybrid", 4: "atomic"}
+_MODE_OF_CODE = {0: "pull", 1: "csc", 2: "bucket", 3: "hybrid", 4: "atomic", 5: "bsort"}
 _SIDE: "dict" = {}
 
 
@@ -607,7 +615,9 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
     ordered ogbn-products-sized graph 46 ms against 8 ms csc), but where
     `graph` = (indptr, indices) is given and its pull_locality reaches HYBRID_LOCALITY (k % 4
     == 0, dim % 4 == 0) "hybrid" pulls the dense tiles and runs csc over the rest (that graph:
-    4.7 against 7.4 ms).  "pull", "bucket" and "hybrid" sum in fp64 LDS accumulators: two runs
+    4.7 against 7.4 ms); otherwise "bsort" at k % 4 == 0, k <= 8 when a window of
+    maxk_bsort_window(k) edges holds >= 2 rows per destination bucket on average (ogbn-
+    products k = 8: 2.9 against 3.9 ms for csc, both with the selector stream), else "csc".  "pull", "bucket" and "hybrid" sum in fp64 LDS accumulators: two runs
     agree except in rare fp32 rounding ties; MAXK_BWD_MODE=csc forces the bitwise-
     deterministic form everywhere."""
     mode = mode or os.environ.get("MAXK_BWD_MODE", "auto")
@@ -618,8 +628,8 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
         rows = num_rows if num_rows else num_cols
         D = -1 if dim is None else int(dim)
         code = int(L.maxk_backward_mode_auto(rows, num_cols, num_e, D, int(k), -1.0))
-        if (code == 1 and graph is not None and k % 4 == 0 and num_e > 0
-                and rows <= 256 * 65536):  # csc unless the graph's locality asks for hybrid
+        if (code in (1, 5) and graph is not None and k % 4 == 0 and num_e > 0
+                and rows <= 256 * 65536):  # csc / bsort unless the locality asks for hybrid
             loc = pull_locality(graph[0], graph[1], int(L.maxk_pull_shift(int(k))))
             code = int(L.maxk_backward_mode_auto(rows, num_cols, num_e, D, int(k), loc))
         mode = _MODE_OF_CODE[code]
@@ -652,7 +662,9 @@ def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[s
     if mode == "bucket":
         return bucket_plan(indices, num_cols, k)
     if mode == "bsort":
-        return bsort_plan(indices, num_cols, k)
+        if indptr is None:
+            raise RuntimeError("backward_plan: mode 'bsort' needs indptr=")
+        return bsort_plan(indptr, indices, num_cols, k)
     if mode == "csc":
         return transpose_plan(indices, num_cols)
     return None
@@ -791,8 +803,8 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                 "maxk_sspmm_backward_bucket")
         return out
     if mode == "bsort":
-        bptr, bpos, bdst, wsrc, shift = (plan if plan is not None
-                                         else bsort_plan(indices, num_cols, k))
+        bptr, bpos, bdst, wsrc, wrow, shift = (plan if plan is not None
+                                               else bsort_plan(indptr, indices, num_cols, k))
         if edge_sel is not None:
             _need(edge_sel, "edge_sel", torch.uint8)
             if tuple(edge_sel.shape) != (E, k):
@@ -803,7 +815,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             _capi.check(L.maxk_sspmm_backward_bsort(
                 _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
                 _ptr(cbsr_idx), _ptr(edge_sel), _ptr(bptr), _ptr(bpos), _ptr(bdst), _ptr(wsrc),
-                shift, _ptr(out), num_rows, num_cols, E, D, k, _ptr(ws), ws.numel(),
+                _ptr(wrow), shift, _ptr(out), num_rows, num_cols, E, D, k, _ptr(ws), ws.numel(),
                 _stream(dev)), "maxk_sspmm_backward_bsort")
         return out
     if mode == "atomic":
@@ -851,17 +863,24 @@ def edge_selectors_wanted(k: int) -> bool:
     return mode == "1" or k <= EDGE_SEL_KMAX
 
 
+def edge_selector_mode(indptr: torch.Tensor, indices: torch.Tensor, k: int, num_cols: int,
+                       dim: Optional[int] = None) -> Optional[str]:
+    """The backward mode a forward should write the per-edge selector stream for
+    (spgemm_forward(edge_sel_out=) -> sspmm_backward(edge_sel=, mode=)), or None: the backward
+    resolves to "csc" or "bsort" (large sparse graphs without locality, where phase 1
+    otherwise gathers a 128-B line of the selector table per edge) and
+    edge_selectors_wanted(k).  The stream holds num_e * k bytes until the backward."""
+    if indices.numel() == 0 or not edge_selectors_wanted(k):
+        return None
+    mode = _bwd_mode(None, k, indices.numel(), num_cols, indptr.numel() - 1, dim,
+                     (indptr, indices))
+    return mode if mode in ("csc", "bsort") else None
+
+
 def use_edge_selectors(indptr: torch.Tensor, indices: torch.Tensor, k: int, num_cols: int,
                        dim: Optional[int] = None) -> bool:
-    """Whether a forward should write the per-edge selector stream for its backward
-    (spgemm_forward(edge_sel_out=) -> sspmm_backward(edge_sel=)): the backward resolves to
-    "csc" (large sparse graphs without locality, where phase 1 otherwise gathers a 128-B line of
-    the selector table per edge) and edge_selectors_wanted(k).  The stream holds num_e * k
-    bytes until the backward."""
-    if indices.numel() == 0 or not edge_selectors_wanted(k):
-        return False
-    return _bwd_mode(None, k, indices.numel(), num_cols, indptr.numel() - 1, dim,
-                     (indptr, indices)) == "csc"
+    """Whether a forward should write the per-edge selector stream (edge_selector_mode)."""
+    return edge_selector_mode(indptr, indices, k, num_cols, dim) is not None
 
 
 def edge_selectors(indices: torch.Tensor, cbsr_idx: torch.Tensor,

@@ -58,9 +58,11 @@ SIGNATURES = {
     "maxk_bucket_plan": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "maxk_bsort_window": (_i32, [_i32]),
     "maxk_bsort_plan_workspace_size": (_sz, [_i64, _i64]),
-    "maxk_bsort_plan": (ctypes.c_int, [_p, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p, _sz, _p]),
+    "maxk_bsort_plan": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p,
+                                       _p, _sz, _p]),
     "maxk_sspmm_backward_bsort_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32]),
-    "maxk_sspmm_backward_bsort": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32,
+    "maxk_sspmm_backward_bsort": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                                 _i32,
                                                  _p, _i64, _i64, _i64, _i32, _i32, _p, _sz, _p]),
     "maxk_sspmm_backward_pull_workspace_size": (_sz, [_i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward_pull": (ctypes.c_int, [_p, _p, _p, _p, _p, _i32, _i32, _p, _i64, _i64,

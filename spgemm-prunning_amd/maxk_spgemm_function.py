@@ -75,11 +75,13 @@ def _f32(t):
 
 
 def _edge_sel_for(indptr, indices, k, num_cols, D):
-    """The [E, k] u8 buffer the forward writes each edge's selectors into when the backward
-    will be the csc form (maxk_cuda_kernels.use_edge_selectors), else None."""
-    if not maxk_cuda_kernels.use_edge_selectors(indptr, indices, k, num_cols, D):
-        return None
-    return torch.empty(indices.numel(), k, dtype=torch.uint8, device=indices.device)
+    """(buffer, mode): the [E, k] u8 buffer the forward writes each edge's selectors into
+    when the backward will be a two-phase form reading them ("csc" or "bsort",
+    maxk_cuda_kernels.edge_selector_mode), else (None, None)."""
+    mode = maxk_cuda_kernels.edge_selector_mode(indptr, indices, k, num_cols, D)
+    if mode is None:
+        return None, None
+    return torch.empty(indices.numel(), k, dtype=torch.uint8, device=indices.device), mode
 
 
 class MaxKSpGEMMFunction(Function):
@@ -113,7 +115,7 @@ class MaxKSpGEMMFunction(Function):
                 .unsqueeze(0).expand(V, -1).contiguous()
         indptr = _indptr_for(graph_indptr, warp4_metadata, num_warps, V)
         row_div = _f32(in_degrees)
-        es = _edge_sel_for(indptr, graph_indices, k, V, D)
+        es, ctx.es_mode = _edge_sel_for(indptr, graph_indices, k, V, D)
         out = maxk_cuda_kernels.spgemm_forward(indptr, graph_indices, _f32(graph_values),
                                                sparse_data, sparse_selector, D, row_div=row_div,
                                                edge_sel_out=es)
@@ -138,7 +140,7 @@ class MaxKSpGEMMFunction(Function):
         D = int(dim_origin) if dim_origin is not None else FULL_DIM
         indptr = _indptr_for(graph_indptr, warp4_metadata, num_warps, V)
         row_div = _f32(degrees)
-        es = _edge_sel_for(indptr, graph_indices, k, V, D)
+        es, ctx.es_mode = _edge_sel_for(indptr, graph_indices, k, V, D)
         out = maxk_cuda_kernels.spgemm_forward(indptr, graph_indices, _f32(graph_values), vals,
                                                sel, D, row_div=row_div, edge_sel_out=es)
         ctx.save_for_backward(indptr, graph_indices, graph_values, sel,
@@ -156,10 +158,11 @@ class MaxKSpGEMMFunction(Function):
         g = grad_output.contiguous()
         if g.dtype != torch.float32:
             g = g.float()
-        # with the forward's edge-selector stream the backward is the csc form reading it
+        # with the forward's edge-selector stream the backward is the two-phase form (csc or
+        # bsort) the forward resolved, reading it
         grad_sparse = maxk_cuda_kernels.sspmm_backward(
             indptr, graph_indices, _f32(graph_values), g, sel, row_div=row_div,
-            edge_sel=es if ctx.has_es else None, mode="csc" if ctx.has_es else None)
+            edge_sel=es if ctx.has_es else None, mode=ctx.es_mode if ctx.has_es else None)
         grads = [None] * ctx.n_inputs
         if ctx.mode == "v1":
             V, D = ctx.shape_v1

@@ -188,6 +188,20 @@ def test_backward_mode_resolution():
     assert mk._bwd_mode("auto", 10, **reddit) == "pull"  # one l per lane below k % 4
     assert mk._bwd_mode("auto", 66, **reddit) == "csc"
     assert mk._bwd_mode("auto", 16, **products) == "csc"
+    # k <= 8 on the sparse graph: window-sorted contribution rows (a window of
+    # maxk_bsort_window(k) edges holds >= 2 rows per destination bucket on average)
+    assert mk._bwd_mode("auto", 8, **products) == "bsort"
+    assert mk._bwd_mode("auto", 4, **products, dim=256) == "bsort"
+    assert mk._bwd_mode("auto", 12, **products) == "csc"
+    assert L.maxk_backward_mode_auto(*P, 256, 8, 1.02) == 5   # MAXK_BWD_BSORT
+    assert L.maxk_backward_mode_auto(*P, 256, 8, 2.0) == 3    # locality still asks for hybrid
+    W8, S8 = L.maxk_bsort_window(8), L.maxk_bucket_shift(8)
+    big = W8 * (1 << S8) // 2  # the most columns whose windows keep 2 rows per bucket
+    assert L.maxk_backward_mode_auto(big, big, 50 * big, 256, 8, -1.0) == 5
+    assert L.maxk_backward_mode_auto(big + 1, big + 1, 50 * big, 256, 8, -1.0) == 1
+    assert mk._bwd_mode("bsort", 8, **reddit) == "bsort"
+    with pytest.raises(RuntimeError):
+        mk._bwd_mode("bsort", 6, **reddit)
     # a shard of 1/8 of the rows keeps Reddit's per-row degree: still the pull form
     assert mk._bwd_mode("auto", 16, num_e=14_326_986, num_cols=232_968, num_rows=29_121) == "pull"
     assert mk._bwd_mode("bucket", 16, **reddit) == "bucket"

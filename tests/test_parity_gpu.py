@@ -184,10 +184,12 @@ def test_bsort_plan(mk, cuda, path):
     V = z["row_ptr"].size - 1
     col = z["col_idx"].astype(np.int64)
     for k in (4, 8, 16, 64):
-        bptr, bpos, bdst, wsrc, shift = mk.bsort_plan(T(z["col_idx"], cuda), V, k, cache=False)
+        bptr, bpos, bdst, wsrc, wrow, shift = mk.bsort_plan(T(z["row_ptr"], cuda),
+                                                            T(z["col_idx"], cuda), V, k,
+                                                            cache=False)
         assert shift == mk._lib().maxk_bucket_shift(k)
         W = mk._lib().maxk_bsort_window(k)
-        assert W == min(65536, (160 * 1024 - 16 * 1024) // (4 * k))
+        assert W == min(65536, 160 * 1024 // (4 * k))
         nb = (V + (1 << shift) - 1) >> shift
         perm, pos = bsort_layout(col, k, shift, W, nb)
         order = np.argsort(col >> shift, kind="stable")
@@ -197,6 +199,7 @@ def test_bsort_plan(mk, cuda, path):
         assert np.array_equal(bpos.cpu().numpy(), pos[order])
         assert np.array_equal(wsrc.cpu().numpy().astype(np.int64),
                               perm - np.arange(col.size) // W * W)
+        assert np.array_equal(wrow.cpu().numpy(), np.repeat(np.arange(V), np.diff(z["row_ptr"])))
     assert mk._lib().maxk_bsort_window(6) == -1 and mk._lib().maxk_bsort_window(0) == -1
 
 
@@ -421,6 +424,35 @@ def test_autograd_v4_wrapper_golden(F, cuda, path):
     close(y, z["y_ref"])
     y.backward(T(z["g"], cuda))
     close(tv.grad, z["grad_cbsr_ref"])
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_autograd_sparse_graph_stream(F, mk, cuda, monkeypatch, k):
+    """A sparse graph whose G is too large for the pull (70k rows, average degree 6): the
+    autograd forward writes the edge-selector stream and its backward reads it in the mode
+    "auto" resolves to -- window-sorted ("bsort") at k = 8, csc at k = 16 -- and the input
+    gradient equals the one through the bitwise csc form without the stream."""
+    torch.manual_seed(k)
+    V, D, E = 70_000, 256, 420_000
+    key = torch.unique(torch.randint(0, V, (E,), device=cuda).long() * V
+                       + torch.randint(0, V, (E,), device=cuda).long())
+    src, dst = (key // V).int(), (key % V).int()
+    ip = torch.zeros(V + 1, dtype=torch.int32, device=cuda)
+    ip[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0).int()
+    val = torch.rand(dst.numel(), device=cuda)
+    deg = torch.bincount(src, minlength=V).clamp(min=1).float()
+    assert mk.edge_selector_mode(ip, dst, k, V, D) == ("bsort" if k == 8 else "csc")
+    g = torch.randn(V, D, device=cuda)
+    grads = []
+    for env in ("auto", "csc"):
+        monkeypatch.setenv("MAXK_BWD_MODE", env)
+        monkeypatch.setenv("MAXK_EDGE_SEL", "1" if env == "auto" else "0")
+        torch.manual_seed(0)
+        x = torch.randn(V, D, device=cuda).requires_grad_(True)
+        y = F.maxk_spgemm(dst, val, x, k, graph_indptr=ip, in_degrees=deg, out_degrees=deg)
+        y.backward(g)
+        grads.append(x.grad)
+    close(grads[0], grads[1].cpu().numpy(), tol=1e-5)
 
 
 # --------------------------------------------------------------------------- oracle, edge cases

@@ -48,7 +48,7 @@ for k in a.k:
     cv, ci = mk.topk_cbsr(X, k)
     out = torch.empty(V, k, device=dev)
     es = mk.edge_selectors(col, ci)
-    bplan = mk.bsort_plan(col, V, k)
+    bplan = mk.bsort_plan(row_ptr, col, V, k)
     ref = mk.sspmm_backward(row_ptr, col, val, G, ci, row_div=div, mode="csc", plan=tplan).clone()
     got = mk.sspmm_backward(row_ptr, col, val, G, ci, row_div=div, mode="bsort", plan=bplan,
                             edge_sel=es).clone()
