@@ -30,4 +30,4 @@ for name in ORDER + sorted(set(rows) - set(ORDER)):
     topk = f"{e['topk_ms']:.2f}" if e.get("topk_ms") else ""
     print(f"| {c['graph']} | {c['V']:,} | {c['E'] / 1e6:.1f}M | {c['D']} | {c['k']} | "
           f"{r['value']:.1f} | {e['fwd_ms']:.2f} | {e['bwd_ms']:.2f} ({e['bwd_mode']}) | "
-          f"{r['roofline']['frac']:.2f} | {topk} | {lib} |")
+          f"{e.get('bwd_alg_GBs', r['roofline']['frac'] * 8000) / 8000:.2f} | {topk} | {lib} |")
