@@ -162,6 +162,10 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_TOPK_FENCE_WAIT  // tools only: s_waitcnt lgkmcnt(0) in the four-row top-k's fences
 #define MAXK_TOPK_FENCE_WAIT 0
 #endif
+#ifndef MAXK_FWD_OUT_NT  // forward: non-temporal output row stores (0 never, 1 always, 2 when
+#define MAXK_FWD_OUT_NT 2   // the output exceeds the Infinity Cache)
+#endif
+constexpr size_t kInfinityCacheBytes = 256ull << 20;  // MI355X MALL (MI355X_MICROARCH.md)
 #ifndef MAXK_BSORT_U  // window-sorted phase 1: wave instructions of edges per batch
 #define MAXK_BSORT_U 2
 #endif

@@ -192,6 +192,8 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack4_kernel(const float *__r
 // the next record loads keeps its bytes live through the batch's peak register use.  They are
 // non-temporal (the stream must not push the record lines out of L2), and the pending bytes sit
 // four to a register with the batch position kept wave-uniform.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 template <int KG, int U, bool WIDE, bool EMIT = false>
 struct EdgeWalker {
     static constexpr int G = kWave / KG;  // edges per wave step
@@ -381,7 +383,8 @@ struct EdgeWalker {
 // add (maxk_spgemm_forward_accumulate): dst[0:D] += instead.
 template <int NC>
 __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict__ dst, int D,
-                                          float div, bool scale, int lane, bool add = false) {
+                                          float div, bool scale, int lane, bool add = false,
+                                          bool nt = false) {
     wave_lds_fence();
     if ((D & 3) == 0) {
         for (int j = lane * 4; j < D; j += kWave * 4) {
@@ -410,7 +413,11 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
                 a.z += o.z;
                 a.w += o.w;
             }
-            *reinterpret_cast<float4 *>(&dst[j]) = a;
+            if (nt)  // output rows streamed past the caches (the record lines stay)
+                __builtin_nontemporal_store(
+                    __builtin_bit_cast(f32x4, a), reinterpret_cast<f32x4 *>(&dst[j]));
+            else
+                *reinterpret_cast<float4 *>(&dst[j]) = a;
         }
     } else {
         for (int j = lane; j < D; j += kWave) {
@@ -433,6 +440,8 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
     const float *__restrict__ row_div, float *__restrict__ out, float *__restrict__ slab,
     int32_t *__restrict__ slab_row, int num_rows, int64_t num_e, int D, int DS, int k,
     int chunk, int n_items, int accumulate, uint8_t *__restrict__ esel) {
+    // accumulate: bit 0 adds onto out (maxk_spgemm_forward_accumulate), bit 1 stores the output
+    // rows non-temporally
     constexpr int NC = kWave / KG;  // LDS copies per wave (one per edge group)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wid = threadIdx.x / kWave;
@@ -511,7 +520,7 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
                 for (int j = 0; j < m; ++j) {
                     const float div = row_div ? row_div[r + j] : 1.f;
                     flush_row<1>(acc + j * DS, DS, out + (int64_t)(r + j) * D, D, div,
-                                 row_div != nullptr, lane, accumulate != 0);
+                                 row_div != nullptr, lane, accumulate & 1, accumulate & 2);
                 }
                 r += m;
                 continue;
@@ -525,7 +534,7 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
                                                k, DS - 1, lane, esel);
         const float div = row_div ? row_div[r] : 1.f;
         flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane,
-                      accumulate != 0);
+                      accumulate & 1, accumulate & 2);
         ++r;
     }
 }
@@ -656,11 +665,20 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
         MAXK_LAUNCHED("cbsr_pack_kernel");
     }
     const int nr = (int)num_rows;
+    // Output rows past the Infinity Cache's size are stored non-temporally, so they do not push
+    // the record lines (the forward's random reads) out: ogbn-products k=8 forward emitting the
+    // selector stream 3.62 -> 3.28 ms, k=16 3.79 -> 3.61, plain forwards and Reddit (238 MB of
+    // output) unchanged (profiles/r03/tune/fwd_out_nt.txt).  A cache-sized output keeps plain
+    // stores, so whatever reads it next can still find it there.  MAXK_FWD_OUT_NT: 0 never,
+    // 1 always, 2 (default) by size.
+    const bool big = (double)num_rows * D * 4 > (double)kInfinityCacheBytes;
+    const int flags = (accumulate ? 1 : 0) |
+                      ((MAXK_FWD_OUT_NT == 1 || (MAXK_FWD_OUT_NT == 2 && big)) ? 2 : 0);
     switch (L.kg) {
 #define MAXK_CASE(KGV)                                                                     \
     case KGV:                                                                              \
         launch_fwd<KGV>(L, s, row_ptr, col_idx, edge_val, rec, row_div, out, slab,         \
-                        slab_row, nr, num_e, D, k, accumulate, esel);                      \
+                        slab_row, nr, num_e, D, k, flags, esel);                           \
         break;
         MAXK_CASE(8)
         MAXK_CASE(16)
