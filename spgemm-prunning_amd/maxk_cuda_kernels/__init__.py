@@ -848,15 +848,17 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     return out
 
 
-EDGE_SEL_KMAX = 16
+EDGE_SEL_KMAX = 32
 
 
 def edge_selectors_wanted(k: int) -> bool:
-    """The rule for the per-edge selector stream given a csc backward: k % 4 == 0 and
+    """The rule for the per-edge selector stream given a csc / bsort backward: k % 4 == 0 and
     k <= EDGE_SEL_KMAX by default (MAXK_EDGE_SEL=auto); MAXK_EDGE_SEL=0 never, =1 at every
     k % 4 == 0.  Measured on the ogbn-products-sized graph: the forward that
-    writes the stream takes +0.68 / +0.80 / +1.14 ms at k = 8 / 16 / 32, the csc backward that
-    reads it -1.16 / -1.08 / -1.15 ms -- a net gain up to k = 16, none at 32."""
+    writes the stream takes +0.68 / +0.80 / +0.84 ms at k = 8 / 16 / 32, the csc backward that
+    reads it -1.16 / -1.08 / -1.10 ms -- a net gain up to k = 32 once the forward stores its
+    output rows non-temporally (r03; before that the k = 32 stream cost the forward what it
+    saved), none at 64 (+2.3 / -1.1 ms)."""
     mode = os.environ.get("MAXK_EDGE_SEL", "auto")
     if k % 4 or mode == "0":
         return False
