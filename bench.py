@@ -462,7 +462,7 @@ def main():
     pipelined = world > 1 and shard.pipeline > 1
     # csc / bsort backward: the forward writes each edge's selectors, phase 1 reads them in
     # order (maxk_spgemm_forward_sel / maxk_sspmm_backward_csc_sel / _bsort) where that pays:
-    # k <= 32 by default, MAXK_EDGE_SEL=0/1 off / on (mk.edge_selectors_wanted)
+    # k <= 16 by default, MAXK_EDGE_SEL=0/1 off / on (mk.edge_selectors_wanted)
     es = (torch.empty(El, k, dtype=torch.uint8, device=dev)
           if (not pipelined and args.bwd_mode in ("csc", "bsort") and El > 0
               and mk.edge_selectors_wanted(k)) else None)
