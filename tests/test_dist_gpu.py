@@ -125,3 +125,13 @@ def test_sharded_nccl_one_gpu_per_rank(graph, single, world):
     if torch.cuda.device_count() < world:
         pytest.skip(f"needs {world} GPUs, {torch.cuda.device_count()} visible")
     _run_world(graph, single, world, "nccl")
+
+
+@pytest.mark.parametrize("bwd", ["bsort", "csc"])
+def test_sharded_forced_backward_modes(graph, single, bwd, monkeypatch):
+    """World 2 with every shard's backward forced to the two-phase forms a large sparse graph
+    resolves to (window-sorted at k <= 8, csc above): the shards' column spaces are the padded
+    gathered ones (gather mode) or the compact halos (halo mode), their plans built per shard
+    and pipeline part."""
+    monkeypatch.setenv("MAXK_BWD_MODE", bwd)
+    _run_world(graph, single, 2, "gloo")
