@@ -578,7 +578,9 @@ def main():
         "fwd_alg_GBs": round(B_f / fwd_avg / 1e6, 1), "bwd_alg_GBs": round(B_b / bwd_avg / 1e6, 1),
         "adjoint_rel_err": adj_err, "max_deg": int(deg.max()), "chunk": args.chunk,
         "bwd_mode": args.bwd_mode, "backward_plan_s": round(t_plan, 4),
-        "build_config": build_cfg, "edge_sel_stream": es is not None,
+        "build_config": build_cfg,
+        "edge_sel_stream": es is not None or (pipelined and any(
+            shard._stream(k, D, j) for j in range(shard.pipeline))),
         "fwd_compulsory_GBs": round(C_f / fwd_avg / 1e6, 1),
         "bwd_compulsory_GBs": round(C_b / bwd_avg / 1e6, 1),
     }

@@ -93,6 +93,15 @@ int maxk_spgemm_forward_accumulate(const int32_t *row_ptr, const int32_t *col_id
                                    int64_t num_rows, int64_t num_cols, int64_t num_e,
                                    int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
                                    void *workspace, size_t workspace_bytes, void *stream);
+/* Both: the product added onto out and the edge-selector stream written (the sharded forward's
+ * later pipelined parts, whose backward reads their own part's stream). */
+int maxk_spgemm_forward_accumulate_sel(const int32_t *row_ptr, const int32_t *col_idx,
+                                       const float *edge_val, const float *cbsr_val,
+                                       const uint8_t *cbsr_idx, const float *row_div, float *out,
+                                       int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                       int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                                       void *workspace, size_t workspace_bytes, void *stream,
+                                       uint8_t *edge_sel);
 
 /* ---------------------------------------------------------------------------
  * Backward outer-product sampled SpMM (SSpMM):

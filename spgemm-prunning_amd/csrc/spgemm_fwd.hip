@@ -706,6 +706,26 @@ extern "C" int maxk_spgemm_forward(const int32_t *row_ptr, const int32_t *col_id
                         workspace_bytes, stream, 0);
 }
 
+namespace {
+// The forward writing the edge-selector stream (accumulate: adding onto out).
+int forward_sel(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div, float *out,
+                int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                int32_t dim_k, int32_t chunk_edges, void *workspace, size_t workspace_bytes,
+                void *stream, uint8_t *edge_sel, int accumulate) {
+    MAXK_REQUIRE(num_e == 0 || edge_sel, "edge_sel must not be NULL");
+    const bool direct = dim_k <= kWave && num_cols < (1 << 24) &&
+                        (uint64_t)record_stride(dim_k, num_cols) * (uint64_t)num_cols < (1ull << 32);
+    if (int rc = forward_impl(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out,
+                              num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
+                              workspace_bytes, stream, accumulate, direct ? edge_sel : nullptr))
+        return rc;
+    if (direct || num_e == 0) return MAXK_OK;
+    // past 32-bit record offsets the walker takes 64-bit addresses and does not emit: gather
+    return maxk_edge_selectors(col_idx, cbsr_idx, num_e, dim_k, edge_sel, stream);
+}
+}  // namespace
+
 extern "C" int maxk_spgemm_forward_sel(const int32_t *row_ptr, const int32_t *col_idx,
                                        const float *edge_val, const float *cbsr_val,
                                        const uint8_t *cbsr_idx, const float *row_div, float *out,
@@ -714,16 +734,21 @@ extern "C" int maxk_spgemm_forward_sel(const int32_t *row_ptr, const int32_t *co
                                        void *workspace, size_t workspace_bytes, void *stream,
                                        uint8_t *edge_sel) {
     clear_error();
-    MAXK_REQUIRE(num_e == 0 || edge_sel, "edge_sel must not be NULL");
-    const bool direct = dim_k <= kWave && num_cols < (1 << 24) &&
-                        (uint64_t)record_stride(dim_k, num_cols) * (uint64_t)num_cols < (1ull << 32);
-    if (int rc = forward_impl(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out,
-                              num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
-                              workspace_bytes, stream, 0, direct ? edge_sel : nullptr))
-        return rc;
-    if (direct || num_e == 0) return MAXK_OK;
-    // past 32-bit record offsets the walker takes 64-bit addresses and does not emit: gather
-    return maxk_edge_selectors(col_idx, cbsr_idx, num_e, dim_k, edge_sel, stream);
+    return forward_sel(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out, num_rows,
+                       num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace, workspace_bytes,
+                       stream, edge_sel, 0);
+}
+
+extern "C" int maxk_spgemm_forward_accumulate_sel(
+    const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val, const float *cbsr_val,
+    const uint8_t *cbsr_idx, const float *row_div, float *out, int64_t num_rows, int64_t num_cols,
+    int64_t num_e, int32_t dim_origin, int32_t dim_k, int32_t chunk_edges, void *workspace,
+    size_t workspace_bytes, void *stream, uint8_t *edge_sel) {
+    clear_error();
+    if (num_e == 0) return MAXK_OK;  // adds zeros, writes no selectors
+    return forward_sel(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out, num_rows,
+                       num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace, workspace_bytes,
+                       stream, edge_sel, 1);
 }
 
 extern "C" int maxk_spgemm_forward_accumulate(const int32_t *row_ptr, const int32_t *col_idx,

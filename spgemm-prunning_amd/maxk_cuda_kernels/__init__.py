@@ -204,7 +204,8 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     """out[num_rows, D] = diag(1/row_div) . A . scatter(cbsr)  (CSR A: indptr/indices/values).
     accumulate: out += the product instead (out= required; maxk_spgemm_forward_accumulate).
     edge_sel_out (uint8 [E, k]): also store each edge's selectors, cbsr_idx[indices[e]], for
-    sspmm_backward(..., edge_sel=) (maxk_spgemm_forward_sel)."""
+    sspmm_backward(..., edge_sel=) (maxk_spgemm_forward_sel; with accumulate,
+    maxk_spgemm_forward_accumulate_sel)."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32), (cbsr_val, "input_data", torch.float32),
                      (cbsr_idx, "sparse_selector", torch.uint8)):
@@ -235,16 +236,16 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, num_cols, E, D, k, chunk)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     if edge_sel_out is not None:
-        if accumulate:
-            raise RuntimeError("edge_sel_out and accumulate cannot be combined")
         _need(edge_sel_out, "edge_sel_out", torch.uint8)
         if tuple(edge_sel_out.shape) != (E, k):
             raise RuntimeError("edge_sel_out must be [num_e, k]")
+        fn = L.maxk_spgemm_forward_accumulate_sel if accumulate else L.maxk_spgemm_forward_sel
         with torch.cuda.device(dev):
-            _capi.check(L.maxk_spgemm_forward_sel(
+            _capi.check(fn(
                 _ptr(indptr), _ptr(indices), _ptr(values), _ptr(cbsr_val), _ptr(cbsr_idx),
                 _ptr(row_div), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws),
-                ws.numel(), _stream(dev), _ptr(edge_sel_out)), "maxk_spgemm_forward_sel")
+                ws.numel(), _stream(dev), _ptr(edge_sel_out)),
+                "maxk_spgemm_forward_accumulate_sel" if accumulate else "maxk_spgemm_forward_sel")
         return out
     fn = L.maxk_spgemm_forward_accumulate if accumulate else L.maxk_spgemm_forward
     with torch.cuda.device(dev):

@@ -111,13 +111,26 @@ class _HipKernels:
         self.bwd_mode = bwd_mode  # None: "auto" per shard (or pipeline part)
 
     def spgemm_forward(self, indptr, indices, values, cbsr_val, cbsr_idx, D, row_div=None,
-                       out=None, accumulate=False):
+                       out=None, accumulate=False, edge_sel_out=None):
         return self.mk.spgemm_forward(indptr, indices, values, cbsr_val, cbsr_idx, D,
-                                      row_div=row_div, out=out, accumulate=accumulate)
+                                      row_div=row_div, out=out, accumulate=accumulate,
+                                      edge_sel_out=edge_sel_out)
 
-    def sspmm_backward(self, indptr, indices, values, grad, cbsr_idx, row_div=None, plan=None):
+    def sspmm_backward(self, indptr, indices, values, grad, cbsr_idx, row_div=None, plan=None,
+                       edge_sel=None):
         return self.mk.sspmm_backward(indptr, indices, values, grad, cbsr_idx, row_div=row_div,
-                                      plan=plan, mode=self.bwd_mode)
+                                      plan=plan, mode=self.bwd_mode, edge_sel=edge_sel)
+
+    def stream_mode(self, indptr, indices, k, num_cols, num_rows=None, dim=None):
+        """Whether a (part's) forward should write the edge-selector stream for its backward:
+        the backward this graph resolves to reads one ("csc" / "bsort") and
+        edge_selectors_wanted(k); maxk_cuda_kernels.edge_selector_mode with this backend's
+        mode."""
+        if indices.numel() == 0 or not self.mk.edge_selectors_wanted(k):
+            return False
+        mode = self.mk._bwd_mode(self.bwd_mode, k, indices.numel(), num_cols, num_rows, dim,
+                                 (indptr, indices))
+        return mode in ("csc", "bsort")
 
     def backward_plan(self, indptr, indices, values, num_cols, k, num_rows=None, dim=None):
         return self.mk.backward_plan(indices, num_cols, k, mode=self.bwd_mode, num_rows=num_rows,
@@ -336,30 +349,49 @@ class ShardedMaxK:
             _wait(works[j][0])
             _wait(works[j][1])
             val_j, idx_j = recvs[j]
-            saved.append(idx_j)
             rp, col, val = self.parts[j]
+            # the part's edge-selector stream when its backward reads one (csc / bsort)
+            es = (torch.empty(col.numel(), k, dtype=torch.uint8, device=dev)
+                  if self._stream(k, D, j) else None)
+            kw = {} if es is None else {"edge_sel_out": es}
+            saved.append((idx_j, es))
             if j == 0:  # writes every row (zeros where part 0 has no edges)
+                if y is not None:
+                    kw["out"] = y
                 y = self.kernels.spgemm_forward(rp, col, val, val_j, idx_j, D,
-                                                row_div=row_div_local,
-                                                **({} if y is None else {"out": y}))
+                                                row_div=row_div_local, **kw)
             elif col.numel() > 0:
                 self.kernels.spgemm_forward(rp, col, val, val_j, idx_j, D, row_div=row_div_local,
-                                            out=y, accumulate=True)
+                                            out=y, accumulate=True, **kw)
         return y, saved
+
+    def _stream(self, k: int, D: int, part: int) -> bool:
+        """Whether pipeline part `part` carries an edge-selector stream at (k, D) (decided once,
+        as its plan is)."""
+        key = ("stream", k, D, part)
+        if key not in self._plans:
+            sm = getattr(self.kernels, "stream_mode", None)
+            rp, col, _ = self.parts[part]
+            self._plans[key] = bool(sm is not None and col.numel() > 0 and
+                                    sm(rp, col, k, self.n_cols_part, self.n_local, D))
+        return self._plans[key]
 
     def grad(self, grad_local: torch.Tensor, saved, row_div_local=None) -> torch.Tensor:
         """CBSR gradient of the owned vertices [n_local, k] from aggregate()'s saved state."""
         if self.pipeline == 1:
             return self.backward(grad_local, saved, row_div_local)
         g = grad_local.contiguous()
-        k = saved[0].shape[1]
+        parts = [s if isinstance(s, tuple) else (s, None) for s in saved]
+        k = parts[0][0].shape[1]
         outs, works, keep = [], [], []
         for j in range(self.pipeline):  # part j's reduce-scatter beside part j+1's backward
             rp, col, val = self.parts[j]
+            idx_j, es = parts[j]
             if col.numel() > 0:
-                partial = self.kernels.sspmm_backward(rp, col, val, g, saved[j],
+                partial = self.kernels.sspmm_backward(rp, col, val, g, idx_j,
                                                       row_div=row_div_local,
-                                                      plan=self.plan(k, g.shape[1], j))
+                                                      plan=self.plan(k, g.shape[1], j),
+                                                      **({} if es is None else {"edge_sel": es}))
             else:
                 partial = torch.zeros(self.n_cols_part, k, dtype=g.dtype, device=g.device)
             o = torch.empty(self.vh, k, dtype=g.dtype, device=g.device)
@@ -397,18 +429,20 @@ class ShardedMaxKFunction(Function):
         idx = topk_indices if topk_indices.dtype == torch.uint8 else topk_indices.to(torch.uint8)
         y, saved = shard.aggregate(topk_values.float().contiguous(), idx.contiguous(),
                                    dim_origin, degrees_local)
-        saved = saved if isinstance(saved, list) else [saved]
+        # pipelined: one (selectors, edge-selector stream or None) pair per part, flattened
+        flat = ([t if t is not None else torch.empty(0) for pair in saved for t in pair]
+                if isinstance(saved, list) else [saved])
         ctx.shard = shard
-        ctx.n_saved = len(saved)
-        ctx.save_for_backward(*saved, degrees_local if degrees_local is not None
+        ctx.save_for_backward(*flat, degrees_local if degrees_local is not None
                               else torch.empty(0))
         ctx.has_div = degrees_local is not None
         return y
 
     @staticmethod
     def backward(ctx, grad_output):
-        *saved, deg = ctx.saved_tensors
-        st = saved if ctx.shard.pipeline > 1 else saved[0]
+        *flat, deg = ctx.saved_tensors
+        st = ([(flat[i], flat[i + 1] if flat[i + 1].numel() else None)
+               for i in range(0, len(flat), 2)] if ctx.shard.pipeline > 1 else flat[0])
         g = ctx.shard.grad(grad_output.float(), st, deg if ctx.has_div else None)
         return None, g, None, None, None
 

@@ -87,6 +87,15 @@ def test_forward_accumulate_golden(mk, cuda, path, chunk):
     y2 = mk.spgemm_forward(*parts[1], *args, row_div=div, chunk=chunk, out=y, accumulate=True)
     assert y2 is y
     close(y, z["y_ref"])
+    # the same, the second part also writing its edge-selector stream
+    # (maxk_spgemm_forward_accumulate_sel)
+    es = torch.full((parts[1][1].numel(), args[1].shape[1]), 0xAB, dtype=torch.uint8,
+                    device=cuda)
+    y = mk.spgemm_forward(*parts[0], *args, row_div=div, chunk=chunk)
+    mk.spgemm_forward(*parts[1], *args, row_div=div, chunk=chunk, out=y, accumulate=True,
+                      edge_sel_out=es)
+    close(y, z["y_ref"])
+    assert torch.equal(es, args[1][parts[1][1].long()])
     with pytest.raises(RuntimeError):
         mk.spgemm_forward(*parts[1], *args, accumulate=True)  # needs out=
 
