@@ -104,9 +104,6 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_TOPK_BISECT  // four-row top-k: bisection over [lower bound, max] of the keys
 #define MAXK_TOPK_BISECT 1
 #endif
-#ifndef MAXK_TOPK_INTERP  // four-row top-k: every other bisection probe interpolated
-#define MAXK_TOPK_INTERP 0
-#endif
 #ifndef MAXK_TOPK_LB  // four-row top-k: bit search from a lower bound of the k-th key
 #define MAXK_TOPK_LB 1
 #endif

@@ -352,37 +352,18 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
             // ends a row early in both.
             uint32_t lo = lb, hi = mx;
             bool done = lo == hi;  // rows past the end search too (see `take` below)
-            // MAXK_TOPK_INTERP: every other probe interpolates: with c_lo keys >= lo and c_hi
-            // keys > hi, it aims where the count would cross k + 1/2 if the keys of (lo, hi]
-            // were spread evenly (within one float binade they are nearly so), clamped into
-            // (lo, hi]; the probes between are midpoints, so the search never takes more than
-            // twice bisection's steps.  The answer is the same whatever the probes.
-            uint32_t c_lo = (uint32_t)D, c_hi = 0u;  // count bounds (c_lo: an upper bound at first)
-            bool interp = MAXK_TOPK_INTERP != 0;
             for (;;) {
                 const bool go = !done;
                 if (__ballot(go) == 0) break;
                 const uint32_t d = hi - lo;
-                uint32_t mid = lo + (d >> 1) + (d & 1u);  // in (lo, hi]: >= 1
-                if (interp && c_lo > c_hi) {
-                    const float f = ((float)(c_lo - (uint32_t)k) - 0.5f) / (float)(c_lo - c_hi);
-                    const float off = f * (float)d;
-                    uint32_t o = off < 0.f ? 0u : (off >= (float)d ? d - 1u : (uint32_t)off);
-                    mid = lo + 1u + o;  // in (lo, hi]
-                }
-                interp = MAXK_TOPK_INTERP != 0 && !interp;
+                const uint32_t mid = lo + (d >> 1) + (d & 1u);  // in (lo, hi]: >= 1
                 uint32_t n = 0;  // columns past D hold key 0 < mid: no mask needed
 #pragma unroll
                 for (int t = 0; t < 16; ++t) n += key[t] >= mid ? 1u : 0u;
                 n = row_sum(n);
                 if (go) {
-                    if (n >= (uint32_t)k) {
-                        lo = mid;
-                        c_lo = n;
-                    } else {
-                        hi = mid - 1u;
-                        c_hi = n;
-                    }
+                    if (n >= (uint32_t)k) lo = mid;
+                    else hi = mid - 1u;
                     if (n == (uint32_t)k || lo == hi) done = true;
                 }
             }
