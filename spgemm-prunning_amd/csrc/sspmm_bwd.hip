@@ -1310,87 +1310,6 @@ __global__ __launch_bounds__(1024) void pull_q_kernel(
     pull_flush(acc, tile_out, ti, h, k, kp, shift);
 }
 
-// ---- experimental: destination-grouped pull (tools/pulld_probe.py) -------------------------
-// The pull's tiles with each tile's entries re-sorted by destination (rows in CSR order inside
-// a destination): 16 lanes own one destination at a time and sum its k = 16 slots in registers
-// (fp32, fixed order: no LDS atomics, no parts), one entry per instruction-quarter, the 16
-// lanes gathering the destination's 16 sorted columns of the entry's source row (TA column c
-// holds ranks 4c .. 4c+3, neighbours in one line).  Group g of the tile takes the entries
-// [grp_e[g], grp_e[g+1]) and writes every destination of [grp_d[g], grp_d[g+1]) (the sum, or
-// zeros for one without entries) to tile_out in rank order; pull_reduce_kernel then sums the
-// slices and maps ranks back to l.
-template <int U>
-__global__ __launch_bounds__(1024) void pulld_kernel(
-    const float *__restrict__ Gp, const uint8_t *__restrict__ sel_q,
-    const int32_t *__restrict__ grp_e, const int32_t *__restrict__ grp_d,
-    const uint2 *__restrict__ ent, float *__restrict__ tile_out, int64_t num_cols, int n_buckets,
-    int n_tiles, int rps, int64_t num_rows, int D, int shift) {
-    constexpr int k = 16, NG = 64;
-    __shared__ __attribute__((aligned(16))) uint8_t sel_lds[16 << 11];
-    const int t = MAXK_PULL_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    if (t >= n_tiles) return;
-    const int s = t / n_buckets, j = t % n_buckets;
-    const int64_t r0 = (int64_t)s * rps;
-    const int64_t nr = num_rows - r0 < rps ? num_rows - r0 : rps;
-    const int64_t c0 = (int64_t)j << shift;
-    pull_sel_store(sel_lds, pull_sel_load(sel_q, c0, num_cols, k, k, 0, shift), k, shift);
-    __syncthreads();
-    const auto grs = wave_buffer(Gp + r0 * D, (uint32_t)(nr > 0 ? nr : 0) * (uint32_t)D * 4u);
-    const int lane = lane_id(), g = threadIdx.x / 16, li = threadIdx.x % 16, gb = lane & 48;
-    const int rank = (li & 3) * 4 + (li >> 2);
-    const int x0 = grp_e[t * (NG + 1) + g], x1 = grp_e[t * (NG + 1) + g + 1];
-    int cur = grp_d[t * (NG + 1) + g];
-    const int dend = grp_d[t * (NG + 1) + g + 1];
-    float *to = tile_out + (size_t)t * ((size_t)k << shift);
-    const uint32_t Db = (uint32_t)D * 4u;
-    const int n = x1 - x0;
-    int nmax = n;
-    nmax = max(nmax, __shfl_xor(nmax, 16));
-    nmax = max(nmax, __shfl_xor(nmax, 32));
-    float acc = 0.f;
-    uint2 my = li < n ? ent[x0 + li] : make_uint2(0u, 0u);
-    for (int b = 0; b < nmax; b += 16) {
-        const uint2 nx = b + 16 + li < n ? ent[x0 + b + 16 + li] : make_uint2(0u, 0u);
-#pragma unroll
-        for (int m0 = 0; m0 < 16; m0 += U) {
-            uint32_t ex[U];
-            float w[U], v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int src = (gb + m0 + u) * 4;
-                ex[u] = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)my.x);
-                w[u] = __uint_as_float((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)my.y));
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const bool ok = b + m0 + u < n;
-                const uint32_t c = sel_lds[(ex[u] >> 16) * 16 + rank];
-                const uint32_t off =
-                    ok && c < (uint32_t)D ? (ex[u] & 0xffffu) * Db + c * 4u : 0x80000000u;
-                v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(grs, (int)off, 0, 0));
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (b + m0 + u < n) {
-                    const int d = (int)(ex[u] >> 16);
-                    if (d != cur) {
-                        to[(size_t)cur * k + rank] = acc;
-                        for (int z = cur + 1; z < d; ++z) to[(size_t)z * k + rank] = 0.f;
-                        cur = d;
-                        acc = 0.f;
-                    }
-                    acc = __builtin_fmaf(w[u], v[u], acc);
-                }
-            }
-        }
-        my = nx;
-    }
-    if (cur < dend) {
-        to[(size_t)cur * k + rank] = acc;
-        for (int z = cur + 1; z < dend; ++z) to[(size_t)z * k + rank] = 0.f;
-    }
-}
-
 // grad_cbsr rows of bucket j = the sum of its slices' tiles, in slice order.  With lmap
 // (pull_q_kernel's slot order, k % 4 == 0) slot f of row c goes to l = lmap[c * k + f].
 // Listed tiles (bucket_ptr != nullptr, k % 4 == 0): bucket j's tiles are the list positions
@@ -2201,48 +2120,4 @@ extern "C" int maxk_sspmm_backward_pull_tiles(
     return pull_impl(grad_out, row_div, cbsr_idx, tile_ent, ent, bucket_shift, slices, true,
                      tile_list, n_tiles, bucket_ptr, bucket_tiles, accumulate, grad_cbsr, num_rows, num_cols,
                      num_e, dim_origin, dim_k, workspace, workspace_bytes, stream);
-}
-
-// Experimental (not in include/maxk_hip.h; tools/pulld_probe.py binds it): the pull with
-// destination-grouped tiles, k = 16, D % 4 == 0, G already divided (no row_div).
-// Workspace: tiles x k x 2^shift floats of tile partials, then rank-sorted selectors and lmap.
-extern "C" int maxk_exp_pulld(const float *grad_out, const uint8_t *cbsr_idx,
-                              const int32_t *grp_e, const int32_t *grp_d, const uint32_t *ent,
-                              int32_t bucket_shift, int32_t slices, float *grad_cbsr,
-                              int64_t num_rows, int64_t num_cols, int32_t dim_origin,
-                              int32_t dim_k, int32_t unroll, void *workspace,
-                              size_t workspace_bytes, void *stream) {
-    clear_error();
-    MAXK_REQUIRE(dim_k == 16 && dim_origin % 4 == 0 && bucket_shift <= 11, "k = 16 only");
-    hipStream_t s = as_stream(stream);
-    const int k = dim_k;
-    const int64_t nb = maxk_bucket_count(num_cols, bucket_shift);
-    const int64_t tiles = (int64_t)slices * nb;
-    const int64_t rps = (num_rows + slices - 1) / slices;
-    const size_t tb = (size_t)tiles * ((size_t)k << bucket_shift) * sizeof(float);
-    const size_t nsel = ((size_t)num_cols * k + 255) & ~(size_t)255;
-    MAXK_REQUIRE(workspace && workspace_bytes >= tb + 2 * nsel, "workspace too small");
-    float *tile_out = reinterpret_cast<float *>(workspace);
-    uint8_t *sel_q = reinterpret_cast<uint8_t *>(workspace) + tb;
-    uint8_t *lm = sel_q + nsel;
-    hipLaunchKernelGGL(pull_sel4_kernel, dim3((unsigned)ceil_div(num_cols, kBlock / (k / 4))),
-                       dim3(kBlock), 0, s, cbsr_idx, sel_q, lm, num_cols, k, k, 1);
-    MAXK_LAUNCHED("pull_sel4_kernel");
-    const unsigned grid = (unsigned)(MAXK_PULL_XCD ? xcd_grid(tiles) : tiles);
-    const uint2 *ent2 = reinterpret_cast<const uint2 *>(ent);
-    if (unroll == 8)
-        hipLaunchKernelGGL(pulld_kernel<8>, dim3(grid), dim3(1024), 0, s, grad_out, sel_q, grp_e,
-                           grp_d, ent2, tile_out, num_cols, (int)nb, (int)tiles, (int)rps,
-                           num_rows, dim_origin, bucket_shift);
-    else
-        hipLaunchKernelGGL(pulld_kernel<4>, dim3(grid), dim3(1024), 0, s, grad_out, sel_q, grp_e,
-                           grp_d, ent2, tile_out, num_cols, (int)nb, (int)tiles, (int)rps,
-                           num_rows, dim_origin, bucket_shift);
-    MAXK_LAUNCHED("pulld_kernel");
-    hipLaunchKernelGGL(pull_reduce_kernel,
-                       dim3((unsigned)nb, (unsigned)ceil_div(ceil_div((int64_t)k << bucket_shift, 4), kBlock)),
-                       dim3(kBlock), 0, s, tile_out, lm, grad_cbsr, num_cols, (int)nb, slices, k,
-                       bucket_shift, nullptr, nullptr, 0);
-    MAXK_LAUNCHED("pull_reduce_kernel");
-    return MAXK_OK;
 }
