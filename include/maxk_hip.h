@@ -401,6 +401,12 @@ int maxk_topk_cbsr(const float *x, int64_t ld_x, float *cbsr_val, uint8_t *cbsr_
 int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_val, uint8_t *cbsr_idx,
                       int32_t *idx32, int64_t num_rows, int32_t dim_origin, int32_t dim_k,
                       void *stream);
+/* Rows (over every top-k launch on the current device since the last reset) whose threshold
+ * search took other than dim_k winners -- a kernel bug, never expected.  The kernels count such
+ * rows and never let one write past its own k winner slots (r02's fault: a dead row's extra
+ * winners overwrote another wave's).  Synchronous (waits for the device); reset != 0 zeroes
+ * the count.  The Python binding checks it after every top-k under MAXK_VALIDATE=1. */
+int maxk_topk_error_rows(int64_t *rows, int32_t reset);
 
 /* dense[r,:] = 0; dense[r, cbsr_idx[r,l]] = cbsr_val[r,l]  (all of dense written).
  * Replaces: zeros(V,D).scatter_(1, sel, grad_sparse), maxk_spgemm_function.py:152,175. */

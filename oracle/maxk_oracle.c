@@ -147,6 +147,31 @@ void oracle_sspmm_bwd_pull(const int32_t *t_ptr, const int32_t *t_src, const flo
     }
 }
 
+/*
+ * CSR of A -> CSR of A^T by a counting sort on the host (stable: each column's
+ * sources in row order, the CSC order the reference's generate_meta_csc.py:14-93
+ * side files hold).  t_ptr[num_cols+1], t_src[E] (source rows), t_val[E].  Built
+ * independently of the GPU plans, so a full-size parity check of a backward that
+ * consumes maxk_transpose_plan / maxk_bsort_plan cannot share a plan defect.
+ */
+void oracle_transpose(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                      int64_t num_rows, int64_t num_cols, int32_t *t_ptr, int32_t *t_src,
+                      float *t_val)
+{
+    int64_t *pos = (int64_t *)calloc((size_t)num_cols + 1, sizeof(int64_t));
+    const int64_t E = row_ptr[num_rows];
+    for (int64_t e = 0; e < E; ++e) ++pos[col_idx[e] + 1];
+    for (int64_t c = 0; c < num_cols; ++c) pos[c + 1] += pos[c];
+    for (int64_t c = 0; c <= num_cols; ++c) t_ptr[c] = (int32_t)pos[c];
+    for (int64_t r = 0; r < num_rows; ++r)
+        for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; ++e) {
+            const int64_t t = pos[col_idx[e]]++;
+            t_src[t] = (int32_t)r;
+            t_val[t] = val[e];
+        }
+    free(pos);
+}
+
 /* Order-preserving key of an fp32 value; every NaN maps above +inf, which is
  * how torch.topk ranks NaN (largest). */
 static inline uint32_t topk_key(float x)

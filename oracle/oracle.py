@@ -48,6 +48,7 @@ def lib():
         L.oracle_sspmm_bwd_pull.argtypes = [_i32p, _i32p, _f32p, _f32p, ctypes.c_void_p, _u8p,
                                             _f32p, _i64, _i32, _i32, _i64, _i64]
         L.oracle_topk.argtypes = [_f32p, _f32p, _u8p, _i64, _i32, _i32]
+        L.oracle_transpose.argtypes = [_i32p, _i32p, _f32p, _i64, _i64, _i32p, _i32p, _f32p]
         L.oracle_warp4.argtypes = [_i32p, _i64, _i32, ctypes.c_void_p, _i64]
         L.oracle_warp4.restype = _i64
         L.oracle_scatter_dense.argtypes = [_f32p, _u8p, _f32p, _i64, _i32, _i32]
@@ -109,6 +110,20 @@ def sspmm_bwd(row_ptr, col_idx, val, grad, cbsr_idx, row_div=None, rows=None):
     lib().oracle_sspmm_bwd(row_ptr, col_idx, val, grad, div, cbsr_idx, out, R, C, D, k, r0, r1)
     del keep
     return out
+
+
+def transpose(row_ptr, col_idx, val, num_cols):
+    """CSR of A -> CSR of A^T (t_ptr over columns, t_src = rows, t_val), stable in row order,
+    by the C counting sort (oracle_transpose): seconds at ogbn-products size, and independent
+    of the GPU-built plans it checks."""
+    row_ptr, col_idx, val = _c(row_ptr, np.int32), _c(col_idx, np.int32), _c(val, np.float32)
+    R = row_ptr.shape[0] - 1
+    E = col_idx.shape[0]
+    t_ptr = np.zeros(num_cols + 1, dtype=np.int32)
+    t_src = np.zeros(E, dtype=np.int32)
+    t_val = np.zeros(E, dtype=np.float32)
+    lib().oracle_transpose(row_ptr, col_idx, val, R, num_cols, t_ptr, t_src, t_val)
+    return t_ptr, t_src, t_val
 
 
 def transpose_csr(row_ptr, col_idx, val, V=None):

@@ -86,9 +86,6 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_PULL_MIN_KP_WIDE  // ... and for k >= 32
 #define MAXK_PULL_MIN_KP_WIDE 16
 #endif
-#ifndef MAXK_PULL_ABL  // tuning only (wrong results): 1 no gathers, 2 no LDS adds, 4 row 0, 8 fixed columns, 16 no entries
-#define MAXK_PULL_ABL 0
-#endif
 #ifndef MAXK_PULL_TRANSPOSE  // pull_q_kernel: a quarter's entries interleaved across its quads
 #define MAXK_PULL_TRANSPOSE 1
 #endif
@@ -122,10 +119,6 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_CSC_STAGE  // csc phase 2: an item's csc_eid slots staged in LDS first
 #define MAXK_CSC_STAGE 1
 #endif
-#ifndef MAXK_BWD_ABL  // tuning only (wrong results): 1 phase-1 selectors from a 4096-row table, 2 no T stores but the last,
-                      // 4 csc phase 2 reads T rows in order (no eid), 8 phase-1 T rows stored at hashed rows
-#define MAXK_BWD_ABL 0
-#endif
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif
@@ -155,9 +148,6 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #endif
 #ifndef MAXK_TOPK_ROWS4_KMAX  // ... for k up to this (at most 64; k=64 ties one row per wave)
 #define MAXK_TOPK_ROWS4_KMAX 48
-#endif
-#ifndef MAXK_TOPK_DIAG  // tools only: four-row top-k search state in idx32 instead of indices
-#define MAXK_TOPK_DIAG 0
 #endif
 #ifndef MAXK_TOPK_FENCE_WAIT  // tools only: s_waitcnt lgkmcnt(0) in the four-row top-k's fences
 #define MAXK_TOPK_FENCE_WAIT 0

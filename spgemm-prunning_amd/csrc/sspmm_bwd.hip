@@ -77,7 +77,6 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
     const uint32_t qst = q < k4 ? 16u * q : 0x80000000u;  // store offset term; past the end if idle
     const uint32_t kb = 4u * (uint32_t)k;                    // T row bytes
     auto sel_off = [&](int c) -> int {
-        if (MAXK_BWD_ABL & 1) c &= 4095;  // tuning: selectors from a 4096-row table
         return WIDE ? (int)((uint32_t)c * (uint32_t)k + qsel)
                     : (int)(__umul24((uint32_t)c, (uint32_t)k) + qsel);
     };
@@ -114,16 +113,7 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
             sv[u] = __builtin_amdgcn_raw_buffer_load_b32(
                 srs, ES ? (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel)
                         : sel_off(c[u]), 0, 0);
-        if (pending && (MAXK_BWD_ABL & 8)) {  // tuning: scattered whole-row stores
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t er = (sto - qst) / kb + u * G;  // row within the segment
-                if (q < k4 && er < (uint32_t)n) {
-                    const uint32_t h = ((uint32_t)sb + er) * 2654435761u & ((1u << 26) - 1u);
-                    *reinterpret_cast<u32x4 *>(T + (size_t)h * k + 4 * q) = xp[u];
-                }
-            }
-        } else if (pending && !(MAXK_BWD_ABL & 2)) {
+        if (pending) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0,
@@ -147,18 +137,8 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
         }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        if (MAXK_BWD_ABL & 2) xp[u].x += xp[u].y;  // tuning: keep the products live
-        if (MAXK_BWD_ABL & 8) {
-            const uint32_t er = (sto - qst) / kb + u * G;
-            if (q < k4 && er < (uint32_t)n) {
-                const uint32_t h = ((uint32_t)sb + er) * 2654435761u & ((1u << 26) - 1u);
-                *reinterpret_cast<u32x4 *>(T + (size_t)h * k + 4 * q) = xp[u];
-            }
-            continue;
-        }
+    for (int u = 0; u < U; ++u)
         __builtin_amdgcn_raw_buffer_store_b128(xp[u], trs, (int)(sto + u * G * kb), 0, MAXK_T_AUX);
-    }
 }
 
 // Walk edges [sb, se) (sb < se) of one staged row.  All loads are
@@ -367,7 +347,7 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T, EidAt e
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int64_t t = base + u * RI + g;
-                const int e = (MAXK_BWD_ABL & 4) ? (int)(t < te ? t : tb) : eid(t < te ? t : tb);
+                const int e = eid(t < te ? t : tb);
                 v[u] = T4[(size_t)(uint32_t)e * LR + q];
                 if (t >= te) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
@@ -1078,7 +1058,7 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
     // their gathers get offsets past the G' descriptor (0, no memory access), their weight
     // 0, and their adds (+0.0) go to a lane-private row of the accumulator.  The loop runs
     // an even number of steps; the last issue is never consumed.
-    const int nsteps = base < n_e && !(MAXK_PULL_ABL & 16) ? (n_e - base + stride - 1) / stride : 0;
+    const int nsteps = base < n_e ? (n_e - base + stride - 1) / stride : 0;
     const int idle = (w * kWave + lane) & ((1 << shift) - 1);
 
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1122,35 +1102,24 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            uint32_t ro = ok[u] ? (ex[u] & 0xffffu) * Db : 0x80000000u;
-            if ((MAXK_PULL_ABL & 4) && ok[u]) ro = 0;  // tuning: every entry reads row 0
+            const uint32_t ro = ok[u] ? (ex[u] & 0xffffu) * Db : 0x80000000u;
 #pragma unroll
             for (int i = 0; i < VPL; ++i) {
-                uint32_t c = VPL == 8 ? (uint32_t)(sv[u] >> (8 * i)) & 255u
-                                      : ((uint32_t)sv[u] >> (8 * i)) & 255u;
-                if (MAXK_PULL_ABL & 8) c = 16 * i + 4 * q;  // tuning: 16 contiguous columns
+                const uint32_t c = VPL == 8 ? (uint32_t)(sv[u] >> (8 * i)) & 255u
+                                            : ((uint32_t)sv[u] >> (8 * i)) & 255u;
                 uint32_t off = ro + c * 4u;
                 if (!FULLD) off = c < (uint32_t)D ? off : 0x80000000u;  // past the buffer: 0
-                if (MAXK_PULL_ABL & 1)
-                    v[u][i] = (float)c;
-                else
-                    v[u][i] = __builtin_bit_cast(
-                        float, __builtin_amdgcn_raw_buffer_load_b32(grs, (int)off, 0, 0));
+                v[u][i] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(grs, (int)off, 0, 0));
             }
         }
     };
-    float abl_sum = 0.f;
     auto consume = [&](float(&v)[U][VPL], int(&dc)[U], float(&wc)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             double *a = &acc[dc[u]];
 #pragma unroll
-            for (int i = 0; i < VPL; ++i) {
-                if (MAXK_PULL_ABL & 2)
-                    abl_sum += wc[u] * v[u][i] * (float)dc[u];
-                else
-                    atomicAdd(a + i, (double)(wc[u] * v[u][i]));
-            }
+            for (int i = 0; i < VPL; ++i) atomicAdd(a + i, (double)(wc[u] * v[u][i]));
         }
     };
     if (nsteps > 0) {
@@ -1174,7 +1143,6 @@ __device__ __forceinline__ void pull_q_entries(double *acc, const uint8_t *sel_l
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-    if (MAXK_PULL_ABL & 2) acc[idle] = abl_sum;
 }
 
 // Where tile t's pieces live: its slice's first row and row count, its bucket's first column.

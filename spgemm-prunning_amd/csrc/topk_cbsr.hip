@@ -24,6 +24,10 @@
 namespace maxk {
 namespace {
 
+// Rows whose search took other than k winners since the last reset (a kernel bug; read and
+// reset by maxk_topk_error_rows).  One counter per device.
+__device__ uint32_t g_topk_bad_rows = 0;
+
 __device__ __forceinline__ uint32_t order_key(float x) {
     const uint32_t u = __float_as_uint(x);
     if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0xffffffffu;
@@ -172,12 +176,15 @@ __global__ __launch_bounds__(kBlock) void topk_cbsr_kernel(const T *__restrict__
         if (out_dense && ok[i])  // fused masked dense output (wave-uniform pointer test)
             out_dense[(int64_t)row * D + lane + kWave * i] = take ? v[i] : T(0);
         const uint64_t mt = __ballot(take);
-        const int slot = take ? slot_base + __popcll(mt & lt_mask) : kMaxDim + lane;
+        const int ws = slot_base + __popcll(mt & lt_mask);
+        const int slot = take && ws < k ? ws : kMaxDim + lane;  // never past the k slots
         s_key[wid][slot] = key[i];
         s_val[wid][slot] = v[i];
         s_col[wid][slot] = (uint8_t)(lane + kWave * i);
         slot_base += __popcll(mt);
     }
+    // any other count than k is a search bug: counted for the host (maxk_topk_error_rows)
+    if (lane == 0 && slot_base != k) atomicAdd(&g_topk_bad_rows, 1u);
     wave_lds_fence();
     // rank of winner p among the winners: (key desc, column asc); 4 slots per LDS read
     for (int p = lane; p < k; p += kWave) {
@@ -458,21 +465,11 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
 #pragma unroll
         for (int t = 0; t < 16; ++t) nw += take[t] ? 1u : 0u;
         uint32_t slot = row_prefix_excl(nw);
-#if MAXK_TOPK_DIAG == 1  // tools only: per-row search state in idx32 (its top-k copy not written)
-        {
-            const uint32_t tot = row_sum(nw);
-            if (out_idx32 && live && q == 0) {
-                int32_t *d = out_idx32 + (int64_t)row * k;
-                d[0] = (int32_t)tot;
-                d[1] = (int32_t)thr;
-                d[2] = need;
-                d[3] = ties ? 1 : 0;
-                d[4] = (int32_t)lb;
-                d[5] = (int32_t)mx;
-                d[6] = (int32_t)neq_row;
-            }
-        }
-#endif
+        // A row taking other than k winners is a bug in the search above (r02's dead sub-rows
+        // were one): it is counted for the host (maxk_topk_error_rows), and the compaction
+        // below never writes past the row's k slots, so such a row cannot reach another row's
+        // or another wave's winners.
+        if (live && q == 0 && row_sum(nw) != (uint32_t)k) atomicAdd(&g_topk_bad_rows, 1u);
         wave_lds_fence();  // the previous group's winners are no longer read
         for (int p = k + q; p < k4; p += 16) {
             wkey[p] = 0u;
@@ -480,7 +477,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         }
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            if (take[t]) {
+            if (take[t] && slot < (uint32_t)k) {
                 wkey[slot] = key[t];
                 wval[slot] = sizeof(T) == 4 ? __builtin_bit_cast(uint32_t, (float)v[t])
                                             : (uint32_t)v[t];
@@ -489,19 +486,6 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
             }
         }
         wave_lds_fence();
-#if MAXK_TOPK_DIAG == 3  // tools only: the row's LDS winner region and per-lane slot state,
-                         // into its dense output row (call maxk_topk_cbsr_dense)
-        if (out_dense && live) {
-            uint32_t *dr = reinterpret_cast<uint32_t *>(out_dense + (int64_t)row * D);
-            for (int w = q; w < 3 * k4 && w < 160; w += 16) dr[w] = wkey[w];
-            dr[160 + q] = row_prefix_excl(nw);
-            dr[176 + q] = nw;
-            dr[192 + q] = (uint32_t)(wkey - lds_topk);
-            dr[208 + q] = (uint32_t)(wcol - lds_topk);
-            dr[224 + q] = slot;
-        }
-        wave_lds_fence();
-#endif
         if (live) {
             for (int p = q; p < k; p += 16) {
                 const uint32_t kp = wkey[p], cp = wcol[p];
@@ -521,11 +505,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
                 else
                     out_val[o] = (T)vb;
                 out_idx[o] = (uint8_t)cp;
-                if (out_idx32 && !MAXK_TOPK_DIAG) out_idx32[o] = (int32_t)cp;
-#if MAXK_TOPK_DIAG == 2  // tools only: per LDS slot p, column | rank << 8 | key low 16 << 16
-                if (out_idx32) out_idx32[(int64_t)row * k + p] =
-                    (int32_t)(cp | ((uint32_t)pos << 8) | (kp << 16));
-#endif
+                if (out_idx32) out_idx32[o] = (int32_t)cp;
             }
         }
         wave_lds_fence();  // winners read before the next group's histogram overwrites them
@@ -682,6 +662,22 @@ extern "C" int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_v
                                  int32_t dim_origin, int32_t dim_k, void *stream) {
     return topk_launch<uint8_t>(x, ld_x, cbsr_val, cbsr_idx, idx32, nullptr, num_rows, dim_origin,
                                 dim_k, stream);
+}
+
+extern "C" int maxk_topk_error_rows(int64_t *rows, int32_t reset) {
+    clear_error();
+    MAXK_REQUIRE(rows, "rows must not be NULL");
+    uint32_t v = 0;
+    MAXK_HIP(hipDeviceSynchronize());
+    MAXK_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_topk_bad_rows), sizeof(v), 0,
+                                 hipMemcpyDeviceToHost));
+    if (reset && v) {
+        const uint32_t z = 0;
+        MAXK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_topk_bad_rows), &z, sizeof(z), 0,
+                                   hipMemcpyHostToDevice));
+    }
+    *rows = v;
+    return MAXK_OK;
 }
 
 namespace maxk {

@@ -37,7 +37,7 @@ __all__ = [
     "load_warp4_metadata_csc", "generate_sparse_selector", "benchmark_spmm_maxk",
     "validate_spmm_maxk", "validate_spmm_maxk_backward", "CudaTimer",
     # MI355X additions
-    "topk_cbsr", "cbsr_scatter_dense", "topk_cbsr_dense", "topk_backward",
+    "topk_cbsr", "cbsr_scatter_dense", "topk_cbsr_dense", "topk_backward", "topk_error_rows",
     "build_warp4_metadata", "warp4_to_indptr",
     "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
     "transpose_plan", "bucket_plan", "bsort_plan", "pull_plan", "edge_selector_mode", "backward_plan", "BWD_MODES",
@@ -956,7 +956,28 @@ def topk_cbsr(x: torch.Tensor, k: int, with_int32: bool = False):
     with torch.cuda.device(dev):
         _capi.check(fn(_ptr(x), x.stride(0), _ptr(val), _ptr(idx), _ptr(idx32), V, D, k,
                        _stream(dev)), name)
+    _check_topk_rows(dev, name)
     return (val, idx, idx32) if with_int32 else (val, idx)
+
+
+def topk_error_rows(device=None, reset: bool = True) -> int:
+    """Rows whose top-k search took other than k winners on `device` since the last reset
+    (maxk_topk_error_rows; synchronises the device).  Always 0 unless the kernel has a bug: the
+    kernels count such a row and keep its writes inside its own k winner slots."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    n = ctypes.c_int64(0)
+    with torch.cuda.device(dev):
+        _capi.check(_lib().maxk_topk_error_rows(ctypes.byref(n), 1 if reset else 0),
+                    "maxk_topk_error_rows")
+    return int(n.value)
+
+
+def _check_topk_rows(dev, name):
+    """MAXK_VALIDATE=1: raise if the launch just made left a row with other than k winners."""
+    if _validate_default() and not torch.cuda.is_current_stream_capturing():
+        bad = topk_error_rows(dev)
+        if bad:
+            raise RuntimeError(f"{name}: {bad} rows took other than k winners (kernel bug)")
 
 
 def cuda_topk_maxk(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -1013,6 +1034,7 @@ def topk_cbsr_dense(x: torch.Tensor, k: int):
         _capi.check(_lib().maxk_topk_cbsr_dense(_ptr(x), x.stride(0), _ptr(val), _ptr(idx),
                                                 _ptr(dense), V, D, k, _stream(dev)),
                     "maxk_topk_cbsr_dense")
+    _check_topk_rows(dev, "maxk_topk_cbsr_dense")
     return dense, val, idx
 
 

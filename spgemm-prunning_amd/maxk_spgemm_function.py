@@ -32,6 +32,7 @@ Fixed caller-visible defects of the reference (DESIGN.md "Boundary"):
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional
 
 import torch
@@ -54,9 +55,33 @@ def _require_kernels():
                            f"available: {_IMPORT_ERROR}")
 
 
+_CONVERTED: dict = {}
+
+
+def _converted(src, tag, make):
+    """make(src), cached per source tensor object and version: the backward's plans and the
+    auto mode's locality pass are cached on the identity of the int32 / fp32 tensors they see,
+    so an int64 indptr, a warp4 array or float64 values converted afresh every step would
+    rebuild them (and re-synchronise the host) on every call."""
+    key = (id(src), tag)
+    hit = _CONVERTED.get(key)
+    if hit is not None:
+        ref, ver, out = hit
+        if ref() is src and ver == src._version:
+            return out
+    out = make(src)
+    if out is src:  # nothing converted: the caller's own tensor, no cache entry needed
+        return out
+    if key not in _CONVERTED:
+        weakref.finalize(src, _CONVERTED.pop, key, None)
+    _CONVERTED[key] = (weakref.ref(src), src._version, out)
+    return out
+
+
 def _i32(t):
-    t = t if t.dtype == torch.int32 else t.int()
-    return t.contiguous()
+    if t.dtype == torch.int32 and t.is_contiguous():
+        return t
+    return _converted(t, "i32", lambda u: u.int().contiguous())
 
 
 def _indptr_for(graph_indptr, warp4_metadata, num_warps, num_v):
@@ -64,14 +89,16 @@ def _indptr_for(graph_indptr, warp4_metadata, num_warps, num_v):
         return _i32(graph_indptr)
     if warp4_metadata is None:
         raise RuntimeError("MaxK SpGEMM needs graph_indptr or warp4_metadata")
-    return maxk_cuda_kernels.warp4_to_indptr(warp4_metadata, num_v, num_warps or None)
+    return _converted(warp4_metadata, ("warp4", int(num_v), int(num_warps or 0)),
+                      lambda w: maxk_cuda_kernels.warp4_to_indptr(w, num_v, num_warps or None))
 
 
 def _f32(t):
     if t is None:
         return None
-    t = t.float() if t.dtype != torch.float32 else t
-    return t.contiguous()
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t
+    return _converted(t, "f32", lambda u: u.float().contiguous())
 
 
 def _edge_sel_for(indptr, indices, k, num_cols, D):

@@ -74,19 +74,19 @@ def test_library_build_config_is_default():
 
 
 def test_flagged_build_fails_provenance():
-    """A library built with an ablation macro (wrong results by design) gets a digest that
+    """A library built with a tuning macro (tools/ builds) gets a digest that
     differs from the tree's, so test_library_built_from_tree rejects it (make -n: the digest
     the Makefile would bake in, nothing compiled)."""
     import subprocess
     cmd = ["make", "-n", "-B", "-C", PKG, "OBJDIR=/tmp/maxk_prov_obj", "OUTDIR=/tmp/maxk_prov_lib"]
     out_plain = subprocess.run(cmd, capture_output=True, text=True, check=True).stdout
-    out_abl = subprocess.run(cmd + ["EXTRA_HIPFLAGS=-DMAXK_PULL_ABL=1"], capture_output=True,
+    out_abl = subprocess.run(cmd + ["EXTRA_HIPFLAGS=-DMAXK_PULL_QU=4"], capture_output=True,
                              text=True, check=True).stdout
     dig = lambda out: re.search(r"MAXK_SRC_DIGEST='\"([0-9a-f]+)\"'", out).group(1)  # noqa: E731
     flags = lambda out: re.search(r"MAXK_BUILD_FLAGS='\"([^\"]*)\"'", out).group(1)  # noqa: E731
     assert dig(out_plain) == source_digest()
     assert dig(out_abl) != source_digest()
-    assert flags(out_plain) == "" and flags(out_abl) == "-DMAXK_PULL_ABL=1"
+    assert flags(out_plain) == "" and flags(out_abl) == "-DMAXK_PULL_QU=4"
 
 
 def test_host_side_argument_validation():

@@ -1,14 +1,18 @@
 """GPU: row-level parity at the BASELINE configs' full sizes.
 
 For every config graph (synthetic stand-ins of the published V and E: Reddit at k = 8, 16,
-32, 64; ogbn-products k = 32; ogbn-proteins k = 64; Flickr D = 64, k = 16) the HIP forward
-and backward (the default "auto" modes, with the in/out-degree division the MaxK layers
-use) are compared with the OpenMP oracle on EVERY row -- hub rows split over many work
-items included -- at the north_star bound |hip - oracle| <= 1e-4 * max(1, |oracle|).  This
+32, 64; ogbn-products k = 8, 16, 32, 64; the planted-community ogbn-products-sized graph in
+locality order at k = 32; ogbn-proteins k = 64; Flickr D = 64, k = 16) the HIP forward and
+backward -- every path the default "auto" rule takes on them (pull, csc, the window-sorted
+bsort and csc reading the forward's edge-selector stream, hybrid), with the in/out-degree
+division the MaxK layers use -- are compared with the OpenMP oracle on EVERY row (hub rows
+split over many work items included) at the north_star bound
+|hip - oracle| <= 1e-4 * max(1, |oracle|).  This
 is the reference's own check (direct_kernel_interface.py:221-372: the full graph against the
 library SpMM, max error on non-zero positions), at 1e-4 instead of 1e-3 and on the backward
-too.  The adjoint identity <A X^, G> = <CBSR, GS> is checked alongside, and the top-k
-(values and selectors) on EVERY row against the oracle's top-k, bit-exact; Gaussian rows (a
+too.  The oracle's backward runs over a transpose built on the host (O.transpose), never
+over one of the product's GPU plans.  The adjoint identity <A X^, G> = <CBSR, GS> is
+checked alongside, and the top-k (values and selectors) on EVERY row against the oracle's top-k, bit-exact; Gaussian rows (a
 Linear layer's output, the input the r02 four-row k=48 probe mismatched on) at the
 ogbn-products size for k = 8 .. 64 as well.
 """
@@ -25,8 +29,17 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4
 
 TAIL_FIXTURE = os.path.join(GOLDEN, "topk", "topk_tail_overflow.npz")
-CONFIGS = [("reddit", 256, 8), ("reddit", 256, 16), ("reddit", 256, 32), ("reddit", 256, 64),
-           ("products", 256, 32), ("proteins", 256, 64), ("flickr", 64, 16)]
+# (graph, D, k, route, backward "auto" resolves to): route "stream" is the autograd surface's
+# path on a sparse graph -- the forward writes the edge-selector stream
+# (spgemm_forward(edge_sel_out=)) and the backward reads it in the mode edge_selector_mode
+# names -- "auto" the plain calls.  products_comm_ordered is the planted-community graph in
+# maxk_graph.locality_order, where "auto" picks the hybrid backward.
+CONFIGS = [("reddit", 256, 8, "auto", "pull"), ("reddit", 256, 16, "auto", "pull"),
+           ("reddit", 256, 32, "auto", "pull"), ("reddit", 256, 64, "auto", "pull"),
+           ("products", 256, 8, "stream", "bsort"), ("products", 256, 16, "stream", "csc"),
+           ("products", 256, 32, "auto", "csc"), ("products", 256, 64, "auto", "csc"),
+           ("products_comm_ordered", 256, 32, "auto", "hybrid"),
+           ("proteins", 256, 64, "auto", "pull"), ("flickr", 64, 16, "auto", "pull")]
 _GRAPHS = {}
 
 
@@ -34,7 +47,11 @@ def graph(name, dev):
     import maxk_graph
     if name not in _GRAPHS:
         _GRAPHS.clear()  # one full-size graph resident at a time
-        rp, col = maxk_graph.synthetic_graph(name, device=dev)
+        if name.endswith("_ordered"):
+            rp, col = maxk_graph.synthetic_graph(name[:-len("_ordered")], device=dev)
+            rp, col, _ = maxk_graph.permute_graph(rp, col, maxk_graph.locality_order(rp, col))
+        else:
+            rp, col = maxk_graph.synthetic_graph(name, device=dev)
         _GRAPHS[name] = (rp, col, rp.cpu().numpy(), col.cpu().numpy())
     return _GRAPHS[name]
 
@@ -67,8 +84,10 @@ def check_rows(got, ref, what, chunk=1 << 24):
     return worst
 
 
-@pytest.mark.parametrize("name,D,k", CONFIGS, ids=[f"{n}-D{d}-k{k}" for n, d, k in CONFIGS])
-def test_full_size_rows_against_oracle(cuda, name, D, k):
+@pytest.mark.parametrize("name,D,k,route,mode", CONFIGS,
+                         ids=[f"{n}-D{d}-k{k}-{m}" + ("-stream" if r == "stream" else "")
+                              for n, d, k, r, m in CONFIGS])
+def test_full_size_rows_against_oracle(cuda, name, D, k, route, mode):
     import maxk_cuda_kernels as mk
     rp, col, rp_h, col_h = graph(name, cuda)
     V, E = rp.numel() - 1, col.numel()
@@ -77,9 +96,20 @@ def test_full_size_rows_against_oracle(cuda, name, D, k):
     x = torch.rand(V, D, generator=gen, device=cuda)
     G = torch.rand(V, D, generator=gen, device=cuda)
     deg = torch.clamp(torch.diff(rp).float(), min=1.0)
+    # the backward the default rule picks for this graph, as the layers reach it
+    assert mk._bwd_mode(None, k, E, V, V, D, (rp, col)) == mode
     cv, ci = mk.topk_cbsr(x, k)
-    y = mk.spgemm_forward(rp, col, val, cv, ci, D, row_div=deg, validate=False)
-    gs = mk.sspmm_backward(rp, col, val, G, ci, row_div=deg, validate=False)
+    if route == "stream":
+        assert mk.edge_selector_mode(rp, col, k, V, D) == mode
+        es = torch.empty(E, k, dtype=torch.uint8, device=cuda)
+        y = mk.spgemm_forward(rp, col, val, cv, ci, D, row_div=deg, validate=False,
+                              edge_sel_out=es)
+        gs = mk.sspmm_backward(rp, col, val, G, ci, row_div=deg, validate=False, edge_sel=es,
+                               mode=mode)
+        del es
+    else:
+        y = mk.spgemm_forward(rp, col, val, cv, ci, D, row_div=deg, validate=False)
+        gs = mk.sspmm_backward(rp, col, val, G, ci, row_div=deg, validate=False)
     # adjoint identity on the device, in double: y carries 1/deg of its rows, gs the 1/deg
     # of its source rows, so both sides are <diag(1/deg) A X^, G>
     a = float((y.double() * G.double()).sum())
@@ -95,16 +125,13 @@ def test_full_size_rows_against_oracle(cuda, name, D, k):
     yo = O.spgemm_fwd(rp_h, col_h, val_h, cv_h, ci_h, D, row_div=deg_h)
     check_rows(y.cpu().numpy(), yo, f"{name} k={k} forward")
     del yo, y
-    # backward, every destination: the oracle's pull form over the GPU-built transpose
-    col_ptr, eid = mk.transpose_plan(col, V)
-    src = torch.repeat_interleave(torch.arange(V, device=cuda, dtype=torch.int32),
-                                  torch.diff(rp).long())
-    t_src = src[eid.long()].cpu().numpy()
-    t_val = val[eid.long()].cpu().numpy()
-    del src
-    go = O.sspmm_bwd_pull(col_ptr.cpu().numpy(), t_src, t_val, G.cpu().numpy(), ci_h,
-                          row_div=deg_h)
-    check_rows(gs.cpu().numpy(), go, f"{name} k={k} backward")
+    # backward, every destination: the oracle's pull form over a transpose built on the host
+    # (O.transpose, a C counting sort), so no GPU-built plan (transpose, bucket / bsort, pull or
+    # hybrid) is shared between the backward under test and its check
+    t_ptr, t_src, t_val = O.transpose(rp_h, col_h, val_h, V)
+    go = O.sspmm_bwd_pull(t_ptr, t_src, t_val, G.cpu().numpy(), ci_h, row_div=deg_h)
+    del t_src, t_val
+    check_rows(gs.cpu().numpy(), go, f"{name} k={k} backward ({mode})")
 
 
 _GAUSS = {}

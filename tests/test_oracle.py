@@ -47,6 +47,9 @@ def test_backward_matches_reference_autograd(path):
     tp, ts, tv = O.transpose_csr(z["row_ptr"], z["col_idx"], z["val"])
     gp = O.sspmm_bwd_pull(tp, ts, tv, z["g"], z["topk_idx"], row_div=z["deg"])
     assert close(gp, gs, 1e-6)
+    V = z["row_ptr"].size - 1
+    tc = O.transpose(z["row_ptr"], z["col_idx"], z["val"], V)  # the C counting sort
+    assert all(np.array_equal(a, b) for a, b in zip(tc, (tp, ts, tv)))
     dense = O.scatter_dense(gs, z["topk_idx"], int(z["D"]))
     assert np.array_equal(np.take_along_axis(dense, z["topk_idx"].astype(np.int64), 1), gs)
     assert np.count_nonzero(dense) <= gs.size

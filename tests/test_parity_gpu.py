@@ -464,6 +464,51 @@ def test_autograd_sparse_graph_stream(F, mk, cuda, monkeypatch, k):
     close(grads[0], grads[1].cpu().numpy(), tol=1e-5)
 
 
+def test_autograd_plans_built_once(F, mk, cuda, monkeypatch):
+    """Steps through the warp4 call shape with int64 indices and float64 weights (each call's
+    int32 / fp32 conversions are cached per source tensor): on a sparse graph where
+    "auto" picks the window-sorted backward at k = 8, the bsort plan and the locality pass are
+    built on the first step only, and every step's gradient is the same."""
+    monkeypatch.delenv("MAXK_BWD_MODE", raising=False)
+    monkeypatch.delenv("MAXK_EDGE_SEL", raising=False)
+    torch.manual_seed(3)
+    V, D, E, k = 70_000, 256, 420_000, 8
+    key = torch.unique(torch.randint(0, V, (E,), device=cuda).long() * V
+                       + torch.randint(0, V, (E,), device=cuda).long())
+    src, dst = key // V, key % V  # int64
+    ip = torch.zeros(V + 1, dtype=torch.int64, device=cuda)
+    ip[1:] = torch.cumsum(torch.bincount(src, minlength=V), 0)
+    val = torch.rand(dst.numel(), device=cuda, dtype=torch.float64)
+    deg = torch.bincount(src, minlength=V).clamp(min=1).double()
+    w = F.MaxKSpmmWrapper("plans")
+    assert w.build_metadata(ip)
+    w._indptr_cache = None  # force the warp4 -> indptr route on every call
+    built = []
+    real = mk.bsort_plan
+
+    def spy(indptr, indices, num_cols, kk, cache=True):
+        n = len(mk._BSORT_CACHE)
+        plan = real(indptr, indices, num_cols, kk, cache)
+        built.append(len(mk._BSORT_CACHE) > n)
+        return plan
+    monkeypatch.setattr(mk, "bsort_plan", spy)
+    tv = torch.rand(V, k, device=cuda)
+    ti = torch.stack([torch.randperm(D, device=cuda)[:k] for _ in range(4)]).repeat(V // 4, 1)
+    g = torch.randn(V, D, device=cuda)
+    loc0 = len(mk._LOCALITY)
+    grads = []
+    for _ in range(3):
+        x = tv.clone().requires_grad_(True)
+        y = F.maxk_spgemm(dst, val, x, ti, w.warp4_metadata, w.num_warps, None, deg,
+                          dim_origin=D)
+        y.backward(g)
+        grads.append(x.grad)
+    assert built == [True, False, False], built
+    assert len(mk._LOCALITY) == loc0 + 1
+    assert torch.equal(grads[0], grads[1]) or close(grads[1], grads[0].cpu().numpy(), 1e-6)
+    close(grads[2], grads[0].cpu().numpy(), 1e-6)
+
+
 # --------------------------------------------------------------------------- oracle, edge cases
 def rand_graph(rng, V, avg, hubs=(), empty=0, cols=None):
     cols = V if cols is None else cols
@@ -745,6 +790,46 @@ def test_topk_threshold_search_edges(mk, cuda, D):
         cv, ci = O.topk(x, k)
         assert np.array_equal(i.cpu().numpy(), ci), (D, k)
         assert np.array_equal(v.cpu().numpy().view(np.uint32), cv.view(np.uint32)), (D, k)
+
+
+@pytest.mark.parametrize("D", [7, 64, 100])
+@pytest.mark.parametrize("tail", [1, 2, 3])
+def test_topk_grid_stride_tails(mk, cuda, D, tail):
+    """The top-k winner compaction over several grid-stride rounds with a last row group of
+    1-3 live rows (V % 4 = tail) and three (or one, two) dead sub-rows: r02's fault was such a
+    group's dead rows compacting past their LDS region into the next wave's winners while it was
+    still ranking.  Rows of all-equal keys, +-0, NaN runs, +-inf, few distinct
+    values and random rows, each row's columns shuffled; every row bit-exact against the oracle
+    for k up to D, through both kernels (four rows per wave up to k = 48, one above), the fused
+    dense form too, and the kernels' own count of rows with other than k winners stays 0
+    (maxk_topk_error_rows; MAXK_VALIDATE=1 also checks it after every call)."""
+    rng = np.random.default_rng(100 * D + tail)
+    V = 2 * 262144 + 4 * 1000 + tail  # > 2 rounds of the four-row grid (16384 x 16 rows)
+    base = [np.full(D, 1.5), np.zeros(D), np.where(rng.random(D) < .5, 0.0, -0.0),
+            np.full(D, np.nan), np.where(rng.random(D) < .3, np.nan, 1.0),
+            np.where(rng.random(D) < .5, np.inf, -np.inf), rng.integers(0, 3, D) * 1.0,
+            rng.standard_normal(D)]
+    kinds = rng.integers(0, len(base) + 2, V)  # two kinds of fresh random rows as well
+    x = np.empty((V, D), np.float32)
+    for j, row in enumerate(base):
+        x[kinds == j] = row
+    m = kinds == len(base)
+    x[m] = rng.standard_normal((int(m.sum()), D))
+    m = kinds == len(base) + 1
+    x[m] = rng.integers(-1, 2, (int(m.sum()), D)) * 0.0  # +-0 and 0 only
+    x = rng.permuted(x, axis=1)
+    xt = T(x, cuda)
+    mk.topk_error_rows(cuda)  # start from a zero count
+    for k in sorted({1, 3, D, min(D, 8), min(D, 16), min(D, 32), min(D, 33), min(D, 48),
+                     min(D, 64)}):
+        v, i = mk.topk_cbsr(xt, k)
+        cv, ci = O.topk(x, k)
+        bad = np.nonzero((i.cpu().numpy() != ci).any(1) |
+                         (v.cpu().numpy().view(np.uint32) != cv.view(np.uint32)).any(1))[0]
+        assert bad.size == 0, (D, tail, k, bad[:10])
+        dense, v2, i2 = mk.topk_cbsr_dense(xt, k)
+        assert torch.equal(i2, i) and torch.equal(v2.view(torch.int32), v.view(torch.int32))
+        assert mk.topk_error_rows(cuda) == 0, (D, tail, k)
 
 
 def test_scatter_dense_and_selector_gen(mk, cuda):
