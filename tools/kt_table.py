@@ -17,6 +17,12 @@ REF = {  # (graph, op) -> {k: ratio}, SURVEY.md 6
     ("flickr", "forward"): {16: "≈2.7×"},
     ("flickr", "backward"): {16: "≈4.2×"},
 }
+KS = (8, 16, 32, 64)
+# the reference's headline (README.md:136; averaged as main_runner_direct.py:138-213 does: the
+# mean over graphs with average degree > 50 of the library SpMM time over the MaxK kernel time)
+REF_AVG = {8: 6.93, 16: 5.39, 32: 2.55, 64: 1.46}
+avg = {}  # (op, "default"|"best") -> {k: [ratios]}
+dense_graphs = []
 print("| graph, op | k=8 | k=16 | k=32 | k=64 |")
 print("|---|---|---|---|---|")
 for g in ("reddit", "products", "proteins", "flickr"):
@@ -28,6 +34,13 @@ for g in ("reddit", "products", "proteins", "flickr"):
         continue
     res = {r["k"]: r for r in js[-1]["results"]}
     lib, best = js[-1]["library_spmm_ms"], js[-1]["library_spmm_ms_best"]
+    if js[-1]["E"] / js[-1]["V"] > 50:
+        dense_graphs.append(g)
+        for op, key in (("forward", "speedup_fwd"), ("backward", "speedup_bwd")):
+            for lb, suf in (("default", ""), ("best", "_vs_best")):
+                for k in KS:
+                    if k in res and res[k].get(key + suf):
+                        avg.setdefault((op, lb), {}).setdefault(k, []).append(res[k][key + suf])
     for op, key in (("forward", "speedup_fwd"), ("backward", "speedup_bwd")):
         ours = [f"{res[k][key]:.1f}× ({res[k][key + '_vs_best']:.1f}×)" if k in res else ""
                 for k in (8, 16, 32, 64)]
@@ -39,3 +52,17 @@ for g in ("reddit", "products", "proteins", "flickr"):
               " | ".join(ref.get(k, "") for k in (8, 16, 32, 64)) + " |")
     print(f"<!-- {g}: library SpMM {lib:.2f} ms (ALG_DEFAULT), {best:.2f} ms (best: "
           f"{js[-1]['library_best_alg']}) -->")
+
+if avg:
+    print()
+    print("| average over graphs with average degree > 50 | k=8 | k=16 | k=32 | k=64 |")
+    print("|---|---|---|---|---|")
+    for op in ("forward", "backward"):
+        for lb in ("default", "best"):
+            a = avg.get((op, lb), {})
+            print(f"| ours, {op} vs rocSPARSE {'ALG_DEFAULT' if lb == 'default' else 'best algorithm'}"
+                  f" ({', '.join(dense_graphs)}) | " +
+                  " | ".join(f"{sum(a[k]) / len(a[k]):.2f}× (n={len(a[k])})" if k in a else ""
+                             for k in KS) + " |")
+    print("| reference, A100 vs cuSPARSE (README.md:136) | " +
+          " | ".join(f"{REF_AVG[k]:.2f}×" for k in KS) + " |")

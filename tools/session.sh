@@ -1,0 +1,170 @@
+#!/bin/bash
+# The one driver for GPU-box sessions (replaces r01-r03's one-off scripts, which are in git
+# history: gpu_round.sh, collect_round.sh, presets_r0*.sh, epochs_r0*.sh, kt_r02.sh,
+# r03_*.sh).  Every GPU step runs under its own time limit and the first failure ends the
+# script (set -e); outputs go to gpurun_out/<round>/<step>/.  Run on the box as
+#   gpurun --timeout 1200 -- 'bash tools/session.sh <round> <step> [<step> ...]'
+# and copy what is judged into profiles/<round>/ with `bash tools/session.sh <round> collect`
+# here.  Steps:
+#   tests     pytest -m gpu (the whole GPU suite)
+#   smoke     __graft_entry__.smoke()
+#   bench     the default bench line (BENCH contract), with CPU baselines
+#   stats     rocprofv3 --kernel-trace --stats of a short default bench
+#   pmc       FETCH_SIZE and WRITE_SIZE of the same short bench, one rocprofv3 --pmc pass each
+#   presets   every preset with its denominators (rocSPARSE every algorithm; CPU baselines
+#             with PRESET_CPU=1)
+#   pmccfg    PMC passes of the non-default configurations in $CFGS
+#             ("name:--bench --args name2:..."), keyed by each run's traffic_key
+#   kt        the reference's kernel test (maxk_kernel_test.py) on every config graph, k = 8..64
+#   epochs    3-layer MaxK-SAGE epochs against the rocSPARSE model
+#   collect   (here, not on the box) copy gpurun_out/<round> into profiles/<round> and write
+#             the summaries (kernel stats, PMC traffic.json, presets and kernel-test tables)
+set -eo pipefail
+R=${1:?round, e.g. r04}; shift
+cd "$(dirname "$0")/.."
+O=gpurun_out/$R
+P=profiles/$R
+export TMPDIR=/tmp
+SHORT="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-rocsparse --no-cpu-spmm"
+
+step_tests() {
+  mkdir -p $O
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+    --timeout-method thread > $O/pytest_gpu.log 2>&1
+  tail -2 $O/pytest_gpu.log
+}
+step_smoke() {
+  mkdir -p $O
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  tail -2 $O/smoke.log
+}
+step_bench() {
+  mkdir -p $O
+  timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err
+  cut -c1-400 $O/bench.json
+}
+step_stats() {
+  mkdir -p $O
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv \
+    -- python3 $SHORT > $O/stats_bench.json 2> $O/stats_bench.err
+}
+step_pmc() {
+  mkdir -p $O
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $c -d $O/pmc_$c -o run --output-format csv \
+      -- python3 $SHORT > $O/pmc_$c.json 2> $O/pmc_$c.err
+  done
+}
+preset() {  # preset <name> <bench args...>
+  local name=$1; shift
+  local cpu="--no-cpu-baseline --no-cpu-spmm"
+  [ "${PRESET_CPU:-0}" = 1 ] && cpu="--cpu-seconds 6"
+  timeout -k 10 400 python bench.py $cpu "$@" > $O/presets/$name.json 2> $O/presets/$name.err
+  python - "$O/presets/$name.json" "$name" <<'EOF'
+import json, sys
+d = json.load(open(sys.argv[1])); e = d["extra"]
+print(sys.argv[2], d["value"], e["fwd_ms"], e["bwd_ms"], e["bwd_mode"], e.get("edge_sel_stream"),
+      d["roofline"]["frac"], e.get("rocsparse_spmm_ms"), e.get("rocsparse_spmm_ms_best"))
+EOF
+}
+step_presets() {
+  mkdir -p $O/presets
+  preset reddit
+  for k in 8 32 64; do preset reddit_k$k --k $k; done
+  for m in bucket csc atomic; do preset reddit_$m --bwd-mode $m --no-rocsparse; done
+  for k in 8 16 32 64; do preset products_k$k --graph products --k $k; done
+  preset products_k4 --graph products --k 4 --no-rocsparse
+  preset proteins --graph proteins
+  preset flickr --graph flickr
+  preset products_comm_ordered --graph products_comm --reorder
+}
+step_pmccfg() {
+  mkdir -p $O/pmc_cfg
+  local name="" args="" w
+  flush() {
+    [ -z "$name" ] && return 0
+    for c in FETCH_SIZE WRITE_SIZE; do
+      timeout -k 10 300 rocprofv3 --pmc $c -d $O/pmc_cfg/${name}_$c -o run --output-format csv \
+        -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-cpu-spmm --no-rocsparse \
+        $args > $O/pmc_cfg/${name}_$c.json 2> $O/pmc_cfg/${name}_$c.err
+    done
+    echo "$name done"
+  }
+  for w in ${CFGS:?CFGS=\"name:--args ...\"}; do
+    if [[ "$w" == *:* ]]; then
+      flush
+      name=${w%%:*}; args=${w#*:}
+    else
+      args="$args $w"
+    fi
+  done
+  flush
+}
+step_kt() {
+  mkdir -p $O/kernel_test
+  for g in reddit products proteins; do
+    timeout -k 10 400 python spgemm-prunning_amd/maxk_kernel_test.py $g --k 8 16 32 64 --json \
+      > $O/kernel_test/$g.txt 2> $O/kernel_test/$g.err
+  done
+  timeout -k 10 300 python spgemm-prunning_amd/maxk_kernel_test.py flickr --dim 64 \
+    --k 8 16 32 64 --json > $O/kernel_test/flickr.txt 2> $O/kernel_test/flickr.err
+  python tools/kt_table.py $O/kernel_test
+}
+step_epochs() {
+  mkdir -p $O/train
+  for cfg in "products products" "reddit reddit" "products_comm_ordered products_comm --reorder"; do
+    set -- $cfg; local n=$1; shift
+    timeout -k 10 400 python3 spgemm-prunning_amd/maxk_train_bench.py "$@" > $O/train/$n.json \
+      2> $O/train/$n.err
+    echo "$n $(cat $O/train/$n.json)"
+  done
+}
+step_collect() {
+  mkdir -p $P
+  if [ -f $O/stats/run_kernel_stats.csv ]; then
+    mkdir -p $P/stats_bench
+    cp $O/stats/run_kernel_stats.csv $P/stats_bench/kernel_stats.csv
+    cp $O/stats_bench.json $P/stats_bench/bench.json
+    python tools/stats_summary.py $P/stats_bench/kernel_stats.csv $P/stats_bench/bench.json \
+      > $P/kernel_stats_summary.txt
+  fi
+  [ -f $O/bench.json ] && cp $O/bench.json $P/bench_default.json
+  for f in pytest_gpu.log smoke.log; do [ -f $O/$f ] && cp $O/$f $P/$f; done
+  if [ -f $O/pmc_FETCH_SIZE/run_counter_collection.csv ]; then
+    cp $O/pmc_FETCH_SIZE/run_counter_collection.csv $P/pmc_fetch_size.csv
+    cp $O/pmc_WRITE_SIZE/run_counter_collection.csv $P/pmc_write_size.csv
+    python tools/pmc_summary.py $P/pmc_fetch_size.csv $P/pmc_write_size.csv \
+      --traffic-out $P/traffic.json \
+      --key "$(python -c "import json; print(json.load(open('$O/pmc_FETCH_SIZE.json'))['roofline']['traffic_key'])")" \
+      > $P/pmc_summary.txt
+  fi
+  if [ -d $O/pmc_cfg ]; then
+    for j in $O/pmc_cfg/*_FETCH_SIZE.json; do
+      local n=$(basename $j _FETCH_SIZE.json)
+      python tools/pmc_summary.py $O/pmc_cfg/${n}_FETCH_SIZE/run_counter_collection.csv \
+        $O/pmc_cfg/${n}_WRITE_SIZE/run_counter_collection.csv --traffic-out $P/traffic.json \
+        --key "$(python -c "import json; print(json.load(open('$j'))['roofline']['traffic_key'])")" \
+        > $P/pmc_summary_$n.txt
+    done
+  fi
+  if [ -d $O/presets ]; then
+    mkdir -p $P/presets
+    cp $O/presets/*.json $P/presets/
+    python tools/presets_table.py $P/presets > $P/presets_table.md
+  fi
+  if [ -d $O/kernel_test ]; then
+    mkdir -p $P/kernel_test
+    cp $O/kernel_test/*.txt $P/kernel_test/
+    python tools/kt_table.py $P/kernel_test > $P/kernel_test_table.md
+  fi
+  if [ -d $O/train ]; then
+    mkdir -p $P/train
+    cp $O/train/*.json $P/train/
+  fi
+}
+
+for s in "$@"; do
+  echo "== $s"
+  step_$s
+done
+echo "session $R done: $*"
