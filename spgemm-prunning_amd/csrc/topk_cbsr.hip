@@ -469,7 +469,8 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         // were one): it is counted for the host (maxk_topk_error_rows), and the compaction
         // below never writes past the row's k slots, so such a row cannot reach another row's
         // or another wave's winners.
-        if (live && q == 0 && row_sum(nw) != (uint32_t)k) atomicAdd(&g_topk_bad_rows, 1u);
+        const uint32_t n_won = row_sum(nw);  // DPP: all lanes active, outside any branch
+        if (live && q == 0 && n_won != (uint32_t)k) atomicAdd(&g_topk_bad_rows, 1u);
         wave_lds_fence();  // the previous group's winners are no longer read
         for (int p = k + q; p < k4; p += 16) {
             wkey[p] = 0u;
