@@ -15,6 +15,8 @@
 #             with PRESET_CPU=1)
 #   pmccfg    PMC passes of the non-default configurations in $CFGS
 #             ("name:--bench --args name2:..."), keyed by each run's traffic_key
+#   statscfg  rocprofv3 --kernel-trace --stats of the configurations in $CFGS (as pmccfg);
+#             summaries in gpurun_out/<round>/stats_cfg/<name>.txt
 #   kt        the reference's kernel test (maxk_kernel_test.py) on every config graph, k = 8..64
 #   epochs    3-layer MaxK-SAGE epochs against the rocSPARSE model
 #   collect   (here, not on the box) copy gpurun_out/<round> into profiles/<round> and write
@@ -78,27 +80,43 @@ step_presets() {
   preset flickr --graph flickr
   preset products_comm_ordered --graph products_comm --reorder
 }
-step_pmccfg() {
-  mkdir -p $O/pmc_cfg
-  local name="" args="" w
-  flush() {
-    [ -z "$name" ] && return 0
-    for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 300 rocprofv3 --pmc $c -d $O/pmc_cfg/${name}_$c -o run --output-format csv \
-        -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-cpu-spmm --no-rocsparse \
-        $args > $O/pmc_cfg/${name}_$c.json 2> $O/pmc_cfg/${name}_$c.err
-    done
-    echo "$name done"
-  }
+cfg_loop() {  # cfg_loop <function>: $CFGS "name:--args ..." -> function name "args"
+  local fn=$1 name="" args="" w
   for w in ${CFGS:?CFGS=\"name:--args ...\"}; do
     if [[ "$w" == *:* ]]; then
-      flush
+      [ -n "$name" ] && $fn "$name" "$args"
       name=${w%%:*}; args=${w#*:}
     else
       args="$args $w"
     fi
   done
-  flush
+  [ -n "$name" ] && $fn "$name" "$args"
+  return 0
+}
+stats_one() {
+  local d=$O/stats_cfg
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d/$1 -o run --output-format csv \
+    -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-cpu-spmm --no-rocsparse \
+    $2 > $d/$1.json 2> $d/$1.err
+  python tools/stats_summary.py $d/$1/run_kernel_stats.csv $d/$1.json > $d/$1.txt
+  echo "$1: $(tail -2 $d/$1.txt | tr '\n' ' ')"
+}
+pmc_one() {
+  local c
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $c -d $O/pmc_cfg/${1}_$c -o run --output-format csv \
+      -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-cpu-spmm --no-rocsparse \
+      $2 > $O/pmc_cfg/${1}_$c.json 2> $O/pmc_cfg/${1}_$c.err
+  done
+  echo "$1 done"
+}
+step_pmccfg() {
+  mkdir -p $O/pmc_cfg
+  cfg_loop pmc_one
+}
+step_statscfg() {
+  mkdir -p $O/stats_cfg
+  cfg_loop stats_one
 }
 step_kt() {
   mkdir -p $O/kernel_test
