@@ -326,10 +326,15 @@ def main():
     ap.add_argument("--reorder", action="store_true",
                     help="relabel the graph once by maxk_graph.locality_order (communities "
                          "contiguous) before sharding and timing")
+    ap.add_argument("--edge-sel", default=None, choices=["auto", "0", "1"],
+                    help="the forward's per-edge selector stream for a csc / bsort backward "
+                         "(MAXK_EDGE_SEL: auto = k <= 16, 0 never, 1 always)")
     ap.add_argument("--dist-mode", default="auto", choices=["auto", "gather", "halo"],
                     help="N > 1: all-gather every CBSR row, or exchange only the halo rows "
                          "(auto: halo when every shard's halo is at most 60 %% of the vertices)")
     args = ap.parse_args()
+    if args.edge_sel is not None:
+        os.environ["MAXK_EDGE_SEL"] = args.edge_sel
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -150,7 +150,10 @@ int maxk_sspmm_backward_csc_sel(const int32_t *row_ptr, const int32_t *col_idx,
                                 int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
                                 int32_t chunk_edges, void *workspace, size_t workspace_bytes,
                                 void *stream);
-/* edge_sel[e, l] = cbsr_idx[col_idx[e], l] (dim_k % 4 == 0; both arrays 16-B aligned). */
+/* edge_sel[e, l] = cbsr_idx[col_idx[e], l]: any dim_k in [1, 256] and any alignment (16-B words
+ * when dim_k % 16 == 0 and both arrays are 16-B aligned, 4-B words for % 4 / 4-B aligned, else
+ * bytes) -- also the fallback of maxk_spgemm_forward_sel past 2^24 columns or 4 GiB of records,
+ * so a stream that works on a small graph works on a large one. */
 int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_idx, int64_t num_e,
                         int32_t dim_k, uint8_t *edge_sel, void *stream);
 
@@ -214,6 +217,10 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
  * bucket_ptr / bucket_dst as maxk_bucket_plan, bucket_pos[num_e] the T row of each bucket
  * entry, win_src[num_e] (u16) the edge (relative to its window) whose row T row p holds,
  * edge_row[num_e] the source row of every CSR edge.
+ * Meant for dim_k <= MAXK_BSORT_KMAX (8; the auto rule's limit): W * 4 * dim_k bytes fill the LDS
+ * stage, so larger k leaves fewer rows per window and bucket (k = 16 on ogbn-products: one
+ * row per run, 5.88 ms against 5.07 for csc) down to W = 160 at dim_k = 256, where the mode is
+ * correct (tested) but only slower than csc.
  * Replaces the same reference kernels as maxk_sspmm_backward.
  * ------------------------------------------------------------------------- */
 int32_t maxk_bsort_window(int32_t dim_k); /* -1 unless dim_k % 4 == 0 in [4, 256] */

@@ -1611,7 +1611,8 @@ int csc_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_v
     return launch_slab_fixup<1>(slab, slab_row, grad_cbsr, k, L.n_items, s);
 }
 
-// edge_sel[e * k + l] = cbsr_idx[col_idx[e] * k + l]: 16 B per thread (k % 16 == 0), else 4 B
+// edge_sel[e * k + l] = cbsr_idx[col_idx[e] * k + l]: wb = 16, 4 or 1 bytes per thread (the
+// widest that divides k and both arrays' alignment)
 __global__ __launch_bounds__(kBlock) void edge_sel_kernel(const int32_t *__restrict__ col_idx,
                                                           const uint8_t *__restrict__ cbsr_idx,
                                                           uint8_t *__restrict__ edge_sel,
@@ -1624,8 +1625,10 @@ __global__ __launch_bounds__(kBlock) void edge_sel_kernel(const int32_t *__restr
     const size_t src = (size_t)(uint32_t)col_idx[e] * k + (size_t)w * wb;
     if (wb == 16)
         reinterpret_cast<uint4 *>(edge_sel)[i] = *reinterpret_cast<const uint4 *>(cbsr_idx + src);
-    else
+    else if (wb == 4)
         reinterpret_cast<uint32_t *>(edge_sel)[i] = *reinterpret_cast<const uint32_t *>(cbsr_idx + src);
+    else
+        edge_sel[i] = cbsr_idx[src];
 }
 }  // namespace
 }  // namespace maxk
@@ -1665,14 +1668,14 @@ extern "C" int maxk_sspmm_backward_csc_sel(const int32_t *row_ptr, const int32_t
 extern "C" int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_idx,
                                    int64_t num_e, int32_t dim_k, uint8_t *edge_sel, void *stream) {
     clear_error();
-    MAXK_REQUIRE(dim_k >= 4 && dim_k % 4 == 0 && dim_k <= kMaxDim,
-                 "edge selectors need dim_k %% 4 == 0, got %d", dim_k);
+    MAXK_REQUIRE(dim_k >= 1 && dim_k <= kMaxDim, "dim_k must be in [1,256], got %d", dim_k);
     MAXK_REQUIRE(num_e >= 0 && num_e * (int64_t)dim_k < (1LL << 40), "num_e out of range");
     if (num_e == 0) return MAXK_OK;
     MAXK_REQUIRE(col_idx && cbsr_idx && edge_sel, "pointers must not be NULL");
-    MAXK_REQUIRE(((uintptr_t)edge_sel & 15) == 0 && ((uintptr_t)cbsr_idx & 15) == 0,
-                 "edge_sel / cbsr_idx must be 16-B aligned");
-    const int wb = dim_k % 16 == 0 ? 16 : 4;
+    // any k and alignment: the widest word that divides k and both arrays' alignment (the
+    // _sel entry points accept 4-B aligned streams, and this is their fallback past 2^24 columns)
+    const uintptr_t al = (uintptr_t)edge_sel | (uintptr_t)cbsr_idx;
+    const int wb = dim_k % 16 == 0 && (al & 15) == 0 ? 16 : dim_k % 4 == 0 && (al & 3) == 0 ? 4 : 1;
     const int64_t n_words = num_e * (dim_k / wb);
     hipLaunchKernelGGL(edge_sel_kernel, dim3((unsigned)ceil_div(n_words, kBlock)), dim3(kBlock), 0,
                        as_stream(stream), col_idx, cbsr_idx, edge_sel, n_words, dim_k, wb);

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 import weakref
 from typing import List, Optional, Tuple
 
@@ -523,6 +524,8 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
 
 
 BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid", "bsort")
+BSORT_KMAX = 8  # MAXK_BSORT_KMAX: the auto rule's bsort limit
+_BSORT_WARNED: set = set()  # (id(indptr), k) already warned about
 
 
 _LOCALITY: "dict" = {}
@@ -804,6 +807,11 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                 "maxk_sspmm_backward_bucket")
         return out
     if mode == "bsort":
+        if k > BSORT_KMAX and (id(indptr), k) not in _BSORT_WARNED:
+            _BSORT_WARNED.add((id(indptr), k))
+            warnings.warn(f"backward mode 'bsort' at k={k} > {BSORT_KMAX} (MAXK_BSORT_KMAX): a "
+                          f"window of {int(L.maxk_bsort_window(k))} edges holds few rows per "
+                          "destination bucket; correct, but csc is faster", stacklevel=2)
         bptr, bpos, bdst, wsrc, wrow, shift = (plan if plan is not None
                                                else bsort_plan(indptr, indices, num_cols, k))
         if edge_sel is not None:
@@ -888,8 +896,8 @@ def use_edge_selectors(indptr: torch.Tensor, indices: torch.Tensor, k: int, num_
 
 def edge_selectors(indices: torch.Tensor, cbsr_idx: torch.Tensor,
                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """uint8 [E, k]: edge e's destination selectors, cbsr_idx[indices[e]] (k % 4 == 0), for
-    sspmm_backward(..., edge_sel=) (maxk_edge_selectors)."""
+    """uint8 [E, k]: edge e's destination selectors, cbsr_idx[indices[e]] (any k, any
+    alignment), for sspmm_backward(..., edge_sel=) (maxk_edge_selectors)."""
     _need(indices, "indices", torch.int32)
     _need(cbsr_idx, "sparse_selector", torch.uint8)
     E, k = indices.numel(), cbsr_idx.shape[1]

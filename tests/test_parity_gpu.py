@@ -212,7 +212,8 @@ def test_bsort_plan(mk, cuda, path):
     assert mk._lib().maxk_bsort_window(6) == -1 and mk._lib().maxk_bsort_window(0) == -1
 
 
-@pytest.mark.parametrize("k", [4, 8, 16, 32])
+@pytest.mark.filterwarnings("ignore:backward mode 'bsort'")
+@pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 256])
 def test_bsort_windows_against_oracle(mk, cuda, k):
     """Window-sorted backward on a products-like graph of many windows (hub rows cut by window
     and wave boundaries, empty rows, a rectangular column space): equal to the oracle, and the
@@ -232,6 +233,24 @@ def test_bsort_windows_against_oracle(mk, cuda, k):
     es = mk.edge_selectors(T(col, cuda), T(ci, cuda))
     b = mk.sspmm_backward(*args, row_div=T(div, cuda), mode="bsort", edge_sel=es)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("k", [1, 3, 4, 10, 16, 32])
+@pytest.mark.parametrize("offset", [0, 1, 4])
+def test_edge_selectors_any_k_and_alignment(mk, cuda, k, offset):
+    """maxk_edge_selectors (the forward's stream fallback past 2^24 columns): any k and any
+    alignment of both arrays give cbsr_idx[col_idx] (it had required k % 4 == 0 and
+    16-B alignment while the _sel entry points accept 4-B aligned streams)."""
+    rng = np.random.default_rng(k * 10 + offset)
+    C, E = 1000, 20000
+    col = T(rng.integers(0, C, E).astype(np.int32), cuda)
+    ci_buf = torch.randint(0, 256, (C * k + offset,), dtype=torch.uint8, device=cuda)
+    ci = ci_buf[offset:].view(C, k)
+    es_buf = torch.zeros(E * k + offset, dtype=torch.uint8, device=cuda)
+    es = es_buf[offset:].view(E, k)
+    mk.edge_selectors(col, ci, out=es)
+    assert torch.equal(es, ci[col.long()])
+    assert not es_buf[:offset].any()  # nothing written before the stream
 
 
 @pytest.mark.parametrize("path", CASES, ids=IDS)
