@@ -326,6 +326,9 @@ def main():
     ap.add_argument("--reorder", action="store_true",
                     help="relabel the graph once by maxk_graph.locality_order (communities "
                          "contiguous) before sharding and timing")
+    ap.add_argument("--dist-pipeline", type=int, default=None,
+                    help="N > 1, gather mode: column parts of the pipelined exchange (default: "
+                         "maxk_dist's rule -- 2 when a rank's exchange is >= 64 MiB, else 1)")
     ap.add_argument("--edge-sel", default=None, choices=["auto", "0", "1"],
                     help="the forward's per-edge selector stream for a csc / bsort backward "
                          "(MAXK_EDGE_SEL: auto = k <= 16, 0 never, 1 always)")
@@ -450,7 +453,8 @@ def main():
     if world > 1:
         import maxk_dist
         shard = maxk_dist.ShardedMaxK(row_ptr, col, val, rank, world, device=dev,
-                                      mode=args.dist_mode)
+                                      mode=args.dist_mode, k=k,
+                                      pipeline=args.dist_pipeline)
         v0, v1, vmax, n_cols = shard.v0, shard.v1, shard.vmax, shard.n_cols
         l_row_ptr, l_col, l_val = shard.row_ptr, shard.col_idx, shard.values
         l_X = X[v0:v1]

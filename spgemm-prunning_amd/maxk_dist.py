@@ -140,6 +140,10 @@ class _HipKernels:
 class ShardedMaxK:
     """Rank-local view of a vertex-partitioned graph for the MaxK aggregation.
 
+    k (optional): the CBSR width the shard will carry; with it, "gather" mode pipelines only
+    an exchange of at least PIPELINE_MIN_BYTES per rank and step (without it: PIPELINE parts
+    at world > 1, as before).
+
     mode "gather": column space = padded [world * vmax] (all vertices);
     mode "halo":   column space = this shard's halo (the distinct columns of its edges, in
                    global-id order).  n_cols is its size either way."""
@@ -156,11 +160,18 @@ class ShardedMaxK:
     # covers the halo only); gather otherwise (a randomly labelled graph's halo is nearly
     # every vertex, and one all-gather / reduce-scatter beats all-to-allv of the same bytes)
     HALO_SHARE = 0.6
+    # the pipeline pays only where the exchange is large enough to hide: each part adds two
+    # all-gathers and a reduce-scatter, and a collective costs tens of microseconds however
+    # small.  With the width k known at construction, a shard whose whole-step exchange (CBSR
+    # rows received, k f32 + k u8 each) is below this stays in one part -- Reddit-sized at
+    # N = 8 moves ~16 MB per rank and step (one all-gather and one reduce-scatter instead of
+    # six collectives), ogbn-products-sized ~390 MB (pipelined)
+    PIPELINE_MIN_BYTES = 64 << 20
 
     def __init__(self, row_ptr: torch.Tensor, col_idx: torch.Tensor, values: torch.Tensor,
                  rank: int, world: int, group=None, device=None, kernels=None,
                  bounds: Optional[List[int]] = None, mode: str = "gather",
-                 pipeline: Optional[int] = None):
+                 pipeline: Optional[int] = None, k: Optional[int] = None):
         if mode not in self.MODES:
             raise ValueError(f"mode must be one of {self.MODES}, got {mode!r}")
         self.rank, self.world, self.group = rank, world, group
@@ -196,6 +207,9 @@ class ShardedMaxK:
         # default: pipelined at world > 1; an explicit part count also applies at world 1 (the
         # one-GPU RCCL test runs the async collectives and part kernels that way)
         P = self.PIPELINE if pipeline is None else int(pipeline)
+        if pipeline is None and k is not None and \
+                (world - 1) * self.vmax * 5 * int(k) < self.PIPELINE_MIN_BYTES:
+            P = 1  # latency-bound exchange: one part
         on = mode == "gather" and (world > 1 or pipeline is not None)
         self.pipeline = max(1, min(P, self.vmax)) if on else 1
         if self.pipeline > 1:

@@ -297,3 +297,27 @@ def test_sharded_hip_single_rank_rccl(cuda):
                 assert torch.equal(y.detach(), y2)
     finally:
         dist.destroy_process_group()
+
+
+def test_pipeline_rule_by_exchange_bytes(monkeypatch):
+    """Gather mode pipelines the exchange only where it is large enough to hide (a collective
+    costs tens of microseconds however small): with k known, a rank whose step exchange
+    (world - 1) * vmax * 5k bytes is below PIPELINE_MIN_BYTES keeps one part; without k, or
+    with an explicit part count, the old behaviour.  No collective runs in gather-mode
+    construction, so this needs no process group."""
+    import maxk_dist
+    rng = np.random.default_rng(7)
+    V = 4000
+    deg = rng.integers(1, 20, V)
+    rp = np.zeros(V + 1, np.int64)
+    rp[1:] = np.cumsum(deg)
+    col = rng.integers(0, V, int(rp[-1])).astype(np.int32)
+    args = (torch.from_numpy(rp.astype(np.int32)), torch.from_numpy(col),
+            torch.rand(col.size))
+    mk = lambda **kw: maxk_dist.ShardedMaxK(*args, rank=0, world=8, kernels=object(),  # noqa
+                                            **kw)
+    assert mk().pipeline == 2 and mk(k=16).pipeline == 1 and mk(k=16, pipeline=3).pipeline == 3
+    s = mk(k=16)
+    need = (8 - 1) * s.vmax * 5 * 16
+    monkeypatch.setattr(maxk_dist.ShardedMaxK, "PIPELINE_MIN_BYTES", need)
+    assert mk(k=16).pipeline == 2 and mk(k=15).pipeline == 1
