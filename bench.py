@@ -631,6 +631,9 @@ def main():
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
                       "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
                       "dist_mode": shard.mode, "dist_pipeline": shard.pipeline,
+                      # since r03 the fwd / bwd intervals hold the CBSR / gradient exchange
+                      # (pipelined or not); r02's N > 1 part times held the kernels only
+                      "exchange_in_interval": True,
                       "rows_per_rank_max": vmax,
                       "edges_this_rank0": El, "cols_this_rank0": n_cols,
                       "exchange_bytes_rank0": shard.exchange_bytes(k)})

@@ -122,6 +122,12 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif
+#ifndef MAXK_STREAM_AUX  // cache policy of the read-once streams (CSR col/val, edge-selector
+#define MAXK_STREAM_AUX 0  // stream) in the forward and phase 1: 0 plain, 2 nt
+#endif
+#ifndef MAXK_GROW_NT  // phase 1 / bsort: G rows (read once, in row order) loaded non-temporally
+#define MAXK_GROW_NT 0
+#endif
 #ifndef MAXK_SCATTER_ROWS4  // dense scatter: four rows per wave
 #define MAXK_SCATTER_ROWS4 1
 #endif

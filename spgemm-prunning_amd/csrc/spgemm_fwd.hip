@@ -246,9 +246,10 @@ struct EdgeWalker {
             float w[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + (it * U + u) * 4, 0, 0);
+                c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + (it * U + u) * 4, 0,
+                                                              MAXK_STREAM_AUX);
                 w[u] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + (it * U + u) * 4, 0, 0));
+                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + (it * U + u) * 4, 0, MAXK_STREAM_AUX));
             }
             for (int lb = 0; lb < k; lb += KG) {
                 const int l = lb + l0;
@@ -310,9 +311,10 @@ struct EdgeWalker {
                 const int lo = (base + grp) * 4;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+                    c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0,
+                                                                  MAXK_STREAM_AUX);
                     w[u] = __uint_as_float(
-                        __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
+                        __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, MAXK_STREAM_AUX));
                 }
                 if constexpr (EMIT) {
                     pend.flush(ers, G, grp, n, k, l0);
