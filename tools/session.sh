@@ -15,6 +15,8 @@
 #             with PRESET_CPU=1)
 #   pmccfg    PMC passes of the non-default configurations in $CFGS
 #             ("name:--bench --args name2:..."), keyed by each run's traffic_key
+#   pmcset    counter sets $SETS ("C1 C2;C3 C4", one pass per set) over the configurations in
+#             $CFGS; per-kernel averages in gpurun_out/<round>/pmc_set/<name>.txt
 #   statscfg  rocprofv3 --kernel-trace --stats of the configurations in $CFGS (as pmccfg);
 #             summaries in gpurun_out/<round>/stats_cfg/<name>.txt
 #   kt        the reference's kernel test (maxk_kernel_test.py) on every config graph, k = 8..64
@@ -113,6 +115,26 @@ pmc_one() {
 step_pmccfg() {
   mkdir -p $O/pmc_cfg
   cfg_loop pmc_one
+}
+# pmcset: per configuration of $CFGS, one rocprofv3 --pmc pass per counter set of $SETS
+# (sets separated by ';', each within one pass's block limits), then the per-kernel averages
+# of every counter: gpurun_out/<round>/pmc_set/<name>.txt
+set_one() {
+  local d=$O/pmc_set/$1 i=0 s
+  mkdir -p $d
+  IFS=';' read -ra sets <<< "${SETS:?SETS=\"C1 C2;C3 ...\"}"
+  for s in "${sets[@]}"; do
+    i=$((i+1))
+    timeout -s KILL 120 rocprofv3 --pmc $s -d $d/p$i -o run --output-format csv \
+      -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-cpu-spmm --no-rocsparse \
+      $2 > $d/p$i.json 2> $d/p$i.err
+  done
+  python3 tools/pmc_kernels.py $d > $O/pmc_set/$1.txt
+  echo "$1 done"
+}
+step_pmcset() {
+  mkdir -p $O/pmc_set
+  cfg_loop set_one
 }
 step_statscfg() {
   mkdir -p $O/stats_cfg
