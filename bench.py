@@ -243,7 +243,11 @@ def host_info():
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "cores_used": host_cores(), "torch_threads": torch.get_num_threads()}
+            "cores_used": host_cores(),
+            # the CPU baselines set torch to host_cores() threads for their timed calls and
+            # restore the process default afterwards (torch_threads_default)
+            "torch_threads_baselines": host_cores(),
+            "torch_threads_default": torch.get_num_threads()}
 
 
 def _order(row_ptr, col):
