@@ -410,8 +410,9 @@ int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_val, uint8_t
                       void *stream);
 /* Rows (over every top-k launch on the current device since the last reset) whose threshold
  * search took other than dim_k winners -- a kernel bug, never expected.  The kernels count such
- * rows and never let one write past its own k winner slots (r02's fault: a dead row's extra
- * winners overwrote another wave's).  Synchronous (waits for the device); reset != 0 zeroes
+ * rows, and such a row never writes past its own k winner slots (r02's fault: a dead row's
+ * extra winners overwrote another wave's); its own output row is then undefined.  Synchronous
+ * (waits for the device); reset != 0 zeroes
  * the count.  The Python binding checks it after every top-k under MAXK_VALIDATE=1. */
 int maxk_topk_error_rows(int64_t *rows, int32_t reset);
 

@@ -158,6 +158,12 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_TOPK_FENCE_WAIT  // tools only: s_waitcnt lgkmcnt(0) in the four-row top-k's fences
 #define MAXK_TOPK_FENCE_WAIT 0
 #endif
+#ifndef MAXK_FWD_F64  // forward: long rows summed with fp64 LDS atomics into one copy per wave
+#define MAXK_FWD_F64 0   // (ds_add_f64, no read-modify-write chain); 0: fp32 copies per edge group
+#endif
+#ifndef MAXK_FWD_F64_PROD32
+#define MAXK_FWD_F64_PROD32 0
+#endif
 #ifndef MAXK_FWD_OUT_NT  // forward: non-temporal output row stores (0 never, 1 always, 2 when
 #define MAXK_FWD_OUT_NT 2   // the output exceeds the Infinity Cache)
 #endif

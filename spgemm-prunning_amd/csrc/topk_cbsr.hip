@@ -302,6 +302,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
     int row = (blockIdx.x * kWavesPerBlock + wid) * 4 + sub;
     T vn[16];
     load_row16<T, VEC>(x + (int64_t)(row < num_rows ? row : num_rows - 1) * ld_x, D, q, vn);
+    uint32_t n_bad = 0;  // this lane's rows with other than k winners (lane q == 0 counts)
     for (int rbase = (blockIdx.x * kWavesPerBlock + wid) * 4; rbase < num_rows;
          rbase += stride, row += stride) {
         const bool live = row < num_rows;
@@ -418,6 +419,13 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         // ranking (r02's k = 48 mismatch on row 2186888 of the seed-0 [2449029, 256] Gaussian
         // input).  Searching costs nothing there; a `live` test per key cost 2-3 %.
         const bool ties = neq_row != (uint32_t)need;
+        // The selection below takes (k - need) keys above the threshold plus min(need, neq_row)
+        // equal ones: exactly k whenever 0 <= need <= neq_row, which the search guarantees.  A
+        // row outside that is a bug in the search (r02's dead sub-rows were one): it is counted
+        // for the host (maxk_topk_error_rows) and takes no winners at all, so its compaction
+        // cannot write past its k LDS slots into another row's or another wave's winners, and
+        // the good rows need no per-winner bound check.  Such a row always has ties
+        // (neq_row != need: need < 0 wraps past any count), so the check sits in that branch.
         bool take[16];
         if (__ballot(ties) == 0) {
 #pragma unroll
@@ -438,6 +446,12 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
                     r += eq ? 1u : 0u;
                 }
                 base += row_sum(c);
+            }
+            const bool bad = (uint32_t)need > neq_row;
+            if (__ballot(bad) != 0) {  // never taken unless the search is wrong
+                n_bad += live && q == 0 && bad ? 1u : 0u;
+#pragma unroll
+                for (int t = 0; t < 16; ++t) take[t] = take[t] && !bad;
             }
         }
         if (out_dense && live) {  // fused masked dense output
@@ -464,13 +478,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         uint32_t nw = 0;
 #pragma unroll
         for (int t = 0; t < 16; ++t) nw += take[t] ? 1u : 0u;
-        uint32_t slot = row_prefix_excl(nw);
-        // A row taking other than k winners is a bug in the search above (r02's dead sub-rows
-        // were one): it is counted for the host (maxk_topk_error_rows), and the compaction
-        // below never writes past the row's k slots, so such a row cannot reach another row's
-        // or another wave's winners.
-        const uint32_t n_won = row_sum(nw);  // DPP: all lanes active, outside any branch
-        if (live && q == 0 && n_won != (uint32_t)k) atomicAdd(&g_topk_bad_rows, 1u);
+        uint32_t slot = row_prefix_excl(nw);  // a row's winners fill slots [0, k) (`bad` above)
         wave_lds_fence();  // the previous group's winners are no longer read
         for (int p = k + q; p < k4; p += 16) {
             wkey[p] = 0u;
@@ -478,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         }
 #pragma unroll
         for (int t = 0; t < 16; ++t) {
-            if (take[t] && slot < (uint32_t)k) {
+            if (take[t]) {
                 wkey[slot] = key[t];
                 wval[slot] = sizeof(T) == 4 ? __builtin_bit_cast(uint32_t, (float)v[t])
                                             : (uint32_t)v[t];
@@ -511,6 +519,7 @@ __global__ __launch_bounds__(kBlock) void topk_rows4_kernel(const T *__restrict_
         }
         wave_lds_fence();  // winners read before the next group's histogram overwrites them
     }
+    if (n_bad) atomicAdd(&g_topk_bad_rows, n_bad);  // maxk_topk_error_rows
 }
 
 #ifdef wave_lds_fence

@@ -4,12 +4,23 @@
 set -eo pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r04/fwd_f64
-mkdir -p $O
+mkdir -p $O gpurun_out/r04/topk
+# the top-k with its bad-row check inside the ties branch: tests, then A/B against r03's kernel
+timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py -k "topk" -x -q --timeout 120 \
+  --timeout-method thread > gpurun_out/r04/topk/pytest_topk3.log 2>&1
+tail -1 gpurun_out/r04/topk/pytest_topk3.log
+for rep in 1 2; do for v in base topk_r03; do
+  lib=spgemm-prunning_amd/lib/variants/$v/libmaxk_hip.so
+  [ $v = base ] && lib=spgemm-prunning_amd/lib/libmaxk_hip.so
+  for rows in 232965 2449029; do
+    echo "== $v rows=$rows rep=$rep"
+    MAXK_HIP_LIB=$lib timeout -k 10 120 python tools/topk_ab.py --rows $rows
+  done
+done; done > gpurun_out/r04/topk/topk_ab3.txt 2>&1
 MAXK_HIP_LIB=$PWD/spgemm-prunning_amd/lib/variants/f64/libmaxk_hip.so timeout -k 10 600 \
   python -u -m pytest tests/test_parity_gpu.py tests/test_fuzz_gpu.py -x -q --timeout 120 \
   --timeout-method thread > $O/pytest_f64.log 2>&1
 tail -1 $O/pytest_f64.log
-R=2 timeout -k 10 900 bash tools/ab_bench.sh "base f64" "--k 16" "--k 8" "--k 32" \
-  "--graph products --k 8" "--graph products --k 32" "--graph proteins" "--graph flickr" \
-  > $O/ab.txt 2>&1
+R=1 timeout -k 10 900 bash tools/ab_bench.sh "base f64 f64p" "--k 16" "--k 8" \
+  "--graph products --k 8" "--graph products --k 32" "--graph proteins" > $O/ab.txt 2>&1
 cat $O/ab.txt
