@@ -6,6 +6,7 @@ cd "$(dirname "$0")/.."
 O=gpurun_out/r04/fwd_f64
 mkdir -p $O gpurun_out/r04/topk
 # the top-k with its bad-row check inside the ties branch: tests, then A/B against r03's kernel
+if [ "${TOPK:-1}" = 1 ]; then
 timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py -k "topk" -x -q --timeout 120 \
   --timeout-method thread > gpurun_out/r04/topk/pytest_topk3.log 2>&1
 tail -1 gpurun_out/r04/topk/pytest_topk3.log
@@ -17,6 +18,7 @@ for rep in 1 2; do for v in base topk_r03; do
     MAXK_HIP_LIB=$lib timeout -k 10 120 python tools/topk_ab.py --rows $rows
   done
 done; done > gpurun_out/r04/topk/topk_ab3.txt 2>&1
+fi
 MAXK_HIP_LIB=$PWD/spgemm-prunning_amd/lib/variants/f64/libmaxk_hip.so timeout -k 10 600 \
   python -u -m pytest tests/test_parity_gpu.py tests/test_fuzz_gpu.py -x -q --timeout 120 \
   --timeout-method thread > $O/pytest_f64.log 2>&1
