@@ -499,11 +499,11 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
     wave_lds_fence();
 }
 
-// LDS floats per wave: NC fp32 copies of stride DS (one per edge group), which also hold the
-// fp64 copy of MAXK_FWD_F64 (DS doubles = 2 copies' worth).
-__host__ __device__ constexpr int fwd_copies(int nc) {
-    return MAXK_FWD_F64 && nc < 2 ? 2 : nc;
-}
+// LDS floats per wave: NC fp32 copies of stride DS (one per edge group; the short-row batches
+// use them under MAXK_FWD_F64 too), then MAXK_FWD_F64's fp64 copy (DS doubles = 2 copies'
+// worth).  The fp64 copy must not alias the fp32 ones: their pad / trash columns [D, DS) are
+// never cleared and would land in live fp64 columns.
+__host__ __device__ constexpr int fwd_copies(int nc) { return MAXK_FWD_F64 ? nc + 2 : nc; }
 
 template <int KG, int U, bool WIDE, bool EMIT>
 __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES) void spgemm_fwd_kernel(
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         *reinterpret_cast<float4 *>(&acc[j]) = make_float4(0.f, 0.f, 0.f, 0.f);
     float *acc_g = acc + (lane / KG) * DS;
     // long rows (and a continued hub row): the group copies, or the wave's fp64 copy
-    double *acc64 = reinterpret_cast<double *>(acc);
+    double *acc64 = reinterpret_cast<double *>(acc + NC * DS);
     auto walk = [&](int sb, int se) {
         if constexpr (MAXK_FWD_F64)
             EdgeWalker<KG, U, WIDE, EMIT>::run(AccF64{acc64}, col_idx, edge_val, rec, RS, sb, se,
