@@ -161,6 +161,9 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_FWD_F64  // forward: long rows summed with fp64 LDS atomics into one copy per wave
 #define MAXK_FWD_F64 0   // (ds_add_f64, no read-modify-write chain); 0: fp32 copies per edge group
 #endif
+#ifndef MAXK_FWD_PF  // forward: next batch's columns / weights loaded before this batch's gathers
+#define MAXK_FWD_PF 0
+#endif
 #ifndef MAXK_FWD_F64_PROD32
 #define MAXK_FWD_F64_PROD32 0
 #endif

@@ -332,9 +332,8 @@ struct EdgeWalker {
             const auto ers = wave_buffer(EMIT ? esel + (size_t)(uint32_t)sb * k : nullptr,
                                          EMIT ? (uint32_t)n * (uint32_t)k : 0u);
             Pending pend;
-            for (int base = 0; base < n; base += G * U) {
-                int c[U];
-                float w[U];
+            // a batch's columns and weights (past n the descriptor returns 0: column 0, weight 0)
+            auto load_cw = [&](int base, int (&c)[U], float (&w)[U]) {
                 const int lo = (base + grp) * 4;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
@@ -343,6 +342,20 @@ struct EdgeWalker {
                     w[u] = __uint_as_float(
                         __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, MAXK_STREAM_AUX));
                 }
+            };
+            // MAXK_FWD_PF: the next batch's columns and weights are loaded before this batch's
+            // record gathers (unconditionally: past n they read 0), so a batch waits on one
+            // memory latency instead of two dependent ones
+            int c[U];
+            float w[U];
+            if constexpr (MAXK_FWD_PF) load_cw(0, c, w);
+            for (int base = 0; base < n; base += G * U) {
+                int cn[U];
+                float wn[U];
+                if constexpr (MAXK_FWD_PF)
+                    load_cw(base + G * U, cn, wn);
+                else
+                    load_cw(base, c, w);
                 if constexpr (EMIT) {
                     pend.flush(ers, G, grp, n, k, l0);
                     __builtin_amdgcn_sched_barrier(0);  // the stores stay ahead of the record loads
@@ -368,6 +381,13 @@ struct EdgeWalker {
                         if constexpr (EMIT) pend.keep(u, s[u]);
                     }
                     if constexpr (EMIT) pend.pos = base;
+                }
+                if constexpr (MAXK_FWD_PF) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        c[u] = cn[u];
+                        w[u] = wn[u];
+                    }
                 }
             }
             if constexpr (EMIT) pend.flush(ers, G, grp, n, k, l0);

@@ -19,10 +19,12 @@ for rep in 1 2; do for v in base topk_r03; do
   done
 done; done > gpurun_out/r04/topk/topk_ab3.txt 2>&1
 fi
-MAXK_HIP_LIB=$PWD/spgemm-prunning_amd/lib/variants/f64/libmaxk_hip.so timeout -k 10 600 \
-  python -u -m pytest tests/test_parity_gpu.py tests/test_fuzz_gpu.py -x -q --timeout 120 \
-  --timeout-method thread > $O/pytest_f64.log 2>&1
-tail -1 $O/pytest_f64.log
-R=1 timeout -k 10 900 bash tools/ab_bench.sh "base f64 f64p" "--k 16" "--k 8" \
-  "--graph products --k 8" "--graph products --k 32" "--graph proteins" > $O/ab.txt 2>&1
+for v in f64pf pf; do
+  MAXK_HIP_LIB=$PWD/spgemm-prunning_amd/lib/variants/$v/libmaxk_hip.so timeout -k 10 600 \
+    python -u -m pytest tests/test_parity_gpu.py -x -q --timeout 120 \
+    --timeout-method thread > $O/pytest_$v.log 2>&1
+  echo "$v: $(tail -1 $O/pytest_$v.log)"
+done
+R=1 timeout -k 10 900 bash tools/ab_bench.sh "base f64 f64p pf f64pf" "--k 16" "--k 8" \
+  "--graph products --k 8" "--graph products --k 32" > $O/ab.txt 2>&1
 cat $O/ab.txt
