@@ -122,12 +122,6 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_T_AUX  // cache policy of the contribution stores: 0 plain, 2 nt, 16 sc1
 #define MAXK_T_AUX 2
 #endif
-#ifndef MAXK_STREAM_AUX  // cache policy of the read-once streams (CSR col/val, edge-selector
-#define MAXK_STREAM_AUX 0  // stream) in the forward and phase 1: 0 plain, 2 nt
-#endif
-#ifndef MAXK_GROW_NT  // phase 1 / bsort: G rows (read once, in row order) loaded non-temporally
-#define MAXK_GROW_NT 0
-#endif
 #ifndef MAXK_SCATTER_ROWS4  // dense scatter: four rows per wave
 #define MAXK_SCATTER_ROWS4 1
 #endif
@@ -157,15 +151,6 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #endif
 #ifndef MAXK_TOPK_FENCE_WAIT  // tools only: s_waitcnt lgkmcnt(0) in the four-row top-k's fences
 #define MAXK_TOPK_FENCE_WAIT 0
-#endif
-#ifndef MAXK_FWD_F64  // forward: long rows summed with fp64 LDS atomics into one copy per wave
-#define MAXK_FWD_F64 0   // (ds_add_f64, no read-modify-write chain); 0: fp32 copies per edge group
-#endif
-#ifndef MAXK_FWD_PF  // forward: next batch's columns / weights loaded before this batch's gathers
-#define MAXK_FWD_PF 0
-#endif
-#ifndef MAXK_FWD_F64_PROD32
-#define MAXK_FWD_F64_PROD32 0
 #endif
 #ifndef MAXK_FWD_OUT_NT  // forward: non-temporal output row stores (0 never, 1 always, 2 when
 #define MAXK_FWD_OUT_NT 2   // the output exceeds the Infinity Cache)

@@ -194,32 +194,6 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack4_kernel(const float *__r
 // four to a register with the batch position kept wave-uniform.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// How an edge group adds w * v into its output row at an LDS column (EdgeWalker::run):
-//  AccF32: the group's own fp32 copy of the row, plain ds_read / ds_write (a read-modify-write:
-//    consecutive steps of a batch may hit one column, so each step's read waits for the last);
-//  AccF64 (MAXK_FWD_F64): the wave's single fp64 copy, one ds_add_f64 per value -- no copy per
-//    group (the adds are atomic) and no dependent LDS round trip per step (the atomics return
-//    nothing); each product w * v is exact in fp64 and the row is rounded to fp32 once, at the
-//    flush.  fp64 because ds_add_f32 costs ~22x ds_add_f64 on gfx950 (193 vs 8.8 cycles per
-//    wave instruction, tools/lds_atomic_probe.hip).
-struct AccF32 {
-    float *a;
-    __device__ __forceinline__ void add(int col, float w, float v) const {
-        float *p = &a[col];
-        *p = __builtin_fmaf(w, v, *p);  // one rounding, in every variant
-    }
-};
-struct AccF64 {
-    double *a;
-    __device__ __forceinline__ void add(int col, float w, float v) const {
-#if MAXK_FWD_F64_PROD32  // tuning: the product rounded to fp32 first (fewer live VGPRs)
-        atomicAdd(&a[col], (double)(w * v));
-#else
-        atomicAdd(&a[col], (double)w * (double)v);
-#endif
-    }
-};
-
 template <int KG, int U, bool WIDE, bool EMIT = false>
 struct EdgeWalker {
     static constexpr int G = kWave / KG;  // edges per wave step
@@ -272,10 +246,9 @@ struct EdgeWalker {
             float w[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + (it * U + u) * 4, 0,
-                                                              MAXK_STREAM_AUX);
+                c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + (it * U + u) * 4, 0, 0);
                 w[u] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + (it * U + u) * 4, 0, MAXK_STREAM_AUX));
+                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + (it * U + u) * 4, 0, 0));
             }
             for (int lb = 0; lb < k; lb += KG) {
                 const int l = lb + l0;
@@ -315,8 +288,7 @@ struct EdgeWalker {
     // return 0: column 0, weight 0, so nothing is clamped), the record table at
     // c*RS + 4l (values) and c*RS + 4k + 2l (selectors), one 24-bit multiply-add each.
     // WIDE (tables past 2^24 columns or 4 GiB): 64-bit addresses, clamped loads.
-    template <class Acc>
-    __device__ __forceinline__ static void run(const Acc &acc, const int32_t *__restrict__ col_idx,
+    __device__ __forceinline__ static void run(float *acc_g, const int32_t *__restrict__ col_idx,
                                                const float *__restrict__ edge_val,
                                                const uint8_t *__restrict__ rec, int RS, int sb,
                                                int se, int k, int trash, int lane,
@@ -332,30 +304,16 @@ struct EdgeWalker {
             const auto ers = wave_buffer(EMIT ? esel + (size_t)(uint32_t)sb * k : nullptr,
                                          EMIT ? (uint32_t)n * (uint32_t)k : 0u);
             Pending pend;
-            // a batch's columns and weights (past n the descriptor returns 0: column 0, weight 0)
-            auto load_cw = [&](int base, int (&c)[U], float (&w)[U]) {
+            for (int base = 0; base < n; base += G * U) {
+                int c[U];
+                float w[U];
                 const int lo = (base + grp) * 4;
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0,
-                                                                  MAXK_STREAM_AUX);
+                    c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
                     w[u] = __uint_as_float(
-                        __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, MAXK_STREAM_AUX));
+                        __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
                 }
-            };
-            // MAXK_FWD_PF: the next batch's columns and weights are loaded before this batch's
-            // record gathers (unconditionally: past n they read 0), so a batch waits on one
-            // memory latency instead of two dependent ones
-            int c[U];
-            float w[U];
-            if constexpr (MAXK_FWD_PF) load_cw(0, c, w);
-            for (int base = 0; base < n; base += G * U) {
-                int cn[U];
-                float wn[U];
-                if constexpr (MAXK_FWD_PF)
-                    load_cw(base + G * U, cn, wn);
-                else
-                    load_cw(base, c, w);
                 if constexpr (EMIT) {
                     pend.flush(ers, G, grp, n, k, l0);
                     __builtin_amdgcn_sched_barrier(0);  // the stores stay ahead of the record loads
@@ -377,17 +335,11 @@ struct EdgeWalker {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const bool live = lok && base + u * G + grp < n;
-                        acc.add(live ? min(s[u], trash) : trash, w[u], v[u]);
+                        float *a = &acc_g[live ? min(s[u], trash) : trash];
+                        *a = __builtin_fmaf(w[u], v[u], *a);  // one rounding, in every variant
                         if constexpr (EMIT) pend.keep(u, s[u]);
                     }
                     if constexpr (EMIT) pend.pos = base;
-                }
-                if constexpr (MAXK_FWD_PF) {
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        c[u] = cn[u];
-                        w[u] = wn[u];
-                    }
                 }
             }
             if constexpr (EMIT) pend.flush(ers, G, grp, n, k, l0);
@@ -417,7 +369,10 @@ struct EdgeWalker {
                         s[u] = reinterpret_cast<const uint16_t *>(p + 4 * k)[lc];
                     }
 #pragma unroll
-                    for (int u = 0; u < U; ++u) acc.add(lok ? min(s[u], trash) : trash, w[u], v[u]);
+                    for (int u = 0; u < U; ++u) {
+                        float *a = &acc_g[lok ? min(s[u], trash) : trash];
+                        *a = __builtin_fmaf(w[u], v[u], *a);
+                    }
                 }
             }
         }
@@ -478,53 +433,6 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
     wave_lds_fence();
 }
 
-// flush_row for the fp64 copy (MAXK_FWD_F64): dst[0:D] = (float)acc[0:D] / div ; acc = 0.
-[[maybe_unused]] __device__ __forceinline__ void flush_row64(double *acc, float *__restrict__ dst, int D, float div,
-                                            bool scale, int lane, bool add = false,
-                                            bool nt = false) {
-    wave_lds_fence();
-    if ((D & 3) == 0) {
-        for (int j = lane * 4; j < D; j += kWave * 4) {
-            double2 *p = reinterpret_cast<double2 *>(&acc[j]);
-            const double2 a0 = p[0], a1 = p[1];
-            p[0] = make_double2(0.0, 0.0);
-            p[1] = make_double2(0.0, 0.0);
-            float4 a = make_float4((float)a0.x, (float)a0.y, (float)a1.x, (float)a1.y);
-            if (scale) {
-                a.x = a.x / div;
-                a.y = a.y / div;
-                a.z = a.z / div;
-                a.w = a.w / div;
-            }
-            if (add) {
-                const float4 o = *reinterpret_cast<const float4 *>(&dst[j]);
-                a.x += o.x;
-                a.y += o.y;
-                a.z += o.z;
-                a.w += o.w;
-            }
-            if (nt)
-                __builtin_nontemporal_store(
-                    __builtin_bit_cast(f32x4, a), reinterpret_cast<f32x4 *>(&dst[j]));
-            else
-                *reinterpret_cast<float4 *>(&dst[j]) = a;
-        }
-    } else {
-        for (int j = lane; j < D; j += kWave) {
-            const float a = (float)acc[j];
-            acc[j] = 0.0;
-            dst[j] = (scale ? a / div : a) + (add ? dst[j] : 0.f);
-        }
-    }
-    wave_lds_fence();
-}
-
-// LDS floats per wave: NC fp32 copies of stride DS (one per edge group; the short-row batches
-// use them under MAXK_FWD_F64 too), then MAXK_FWD_F64's fp64 copy (DS doubles = 2 copies'
-// worth).  The fp64 copy must not alias the fp32 ones: their pad / trash columns [D, DS) are
-// never cleared and would land in live fp64 columns.
-__host__ __device__ constexpr int fwd_copies(int nc) { return MAXK_FWD_F64 ? nc + 2 : nc; }
-
 template <int KG, int U, bool WIDE, bool EMIT>
 __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
@@ -543,27 +451,10 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
     const int blk = MAXK_FWD_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int item = blk * kWavesPerBlock + wid;
     if (item >= n_items) return;  // whole wave; no workgroup barrier below
-    constexpr int NCL = fwd_copies(NC);
-    float *acc = lds + (size_t)wid * NCL * DS;
-    for (int j = lane * 4; j < NCL * DS; j += kWave * 4)
+    float *acc = lds + (size_t)wid * NC * DS;
+    for (int j = lane * 4; j < NC * DS; j += kWave * 4)
         *reinterpret_cast<float4 *>(&acc[j]) = make_float4(0.f, 0.f, 0.f, 0.f);
     float *acc_g = acc + (lane / KG) * DS;
-    // long rows (and a continued hub row): the group copies, or the wave's fp64 copy
-    double *acc64 = reinterpret_cast<double *>(acc + NC * DS);
-    auto walk = [&](int sb, int se) {
-        if constexpr (MAXK_FWD_F64)
-            EdgeWalker<KG, U, WIDE, EMIT>::run(AccF64{acc64}, col_idx, edge_val, rec, RS, sb, se,
-                                               k, DS - 1, lane, esel);
-        else
-            EdgeWalker<KG, U, WIDE, EMIT>::run(AccF32{acc_g}, col_idx, edge_val, rec, RS, sb, se,
-                                               k, DS - 1, lane, esel);
-    };
-    auto flush = [&](float *dst, float div, int flags) {
-        if constexpr (MAXK_FWD_F64)
-            flush_row64(acc64, dst, D, div, row_div != nullptr, lane, flags & 1, flags & 2);
-        else
-            flush_row<NC>(acc, DS, dst, D, div, row_div != nullptr, lane, flags & 1, flags & 2);
-    };
 
     const int64_t total = (int64_t)num_rows + num_e;
     const int64_t d0 = (int64_t)item * chunk;
@@ -578,9 +469,10 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         if (d1 - r < se) se = d1 - r;
         if (sb < se) {
             wave_lds_fence();
-            walk((int)sb, (int)se);
+            EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se,
+                                               k, DS - 1, lane, esel);
             const float div = row_div ? row_div[r - 1] : 1.f;
-            flush(slab + (int64_t)item * D, div, 0);
+            flush_row<NC>(acc, DS, slab + (int64_t)item * D, D, div, row_div != nullptr, lane);
             cont = r - 1;
         }
     }
@@ -637,9 +529,12 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         int64_t se = (int64_t)row_ptr[r + 1];
         if (d1 - r - 1 < se) se = d1 - r - 1;
         wave_lds_fence();
-        if (rb < se) walk((int)rb, (int)se);
+        if (rb < se)
+            EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se,
+                                               k, DS - 1, lane, esel);
         const float div = row_div ? row_div[r] : 1.f;
-        flush(out + (int64_t)r * D, div, accumulate);
+        flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane,
+                      accumulate & 1, accumulate & 2);
         ++r;
     }
 }
@@ -687,7 +582,7 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
                 int accumulate, uint8_t *esel) {
     constexpr int U = MAXK_FWD_U;
     constexpr int NC = kWave / KG;
-    const size_t lds = (size_t)kWavesPerBlock * fwd_copies(NC) * L.DS * sizeof(float);
+    const size_t lds = (size_t)kWavesPerBlock * NC * L.DS * sizeof(float);
     const int64_t blocks = ceil_div(L.n_items, kWavesPerBlock);
     const dim3 grid((unsigned)(MAXK_FWD_XCD ? xcd_grid(blocks) : blocks));
     // 32-bit record offsets need c < 2^24 (24-bit multiply) and the table under 4 GiB

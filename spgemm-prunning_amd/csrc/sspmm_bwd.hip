@@ -86,8 +86,8 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
         const int lo = grp * 4;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (!ES) c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, MAXK_STREAM_AUX);
-            w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, MAXK_STREAM_AUX));
+            if (!ES) c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+            w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
         }
     }
     u32x4 xp[U];
@@ -102,9 +102,9 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (!ES)
-                    cn[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, MAXK_STREAM_AUX);
+                    cn[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
                 wn[u] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, MAXK_STREAM_AUX));
+                    __builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
             }
         }
         uint32_t sv[U];
@@ -112,7 +112,7 @@ __device__ __forceinline__ void push_x4(const float *g_lds, const int32_t *__res
         for (int u = 0; u < U; ++u)
             sv[u] = __builtin_amdgcn_raw_buffer_load_b32(
                 srs, ES ? (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel)
-                        : sel_off(c[u]), 0, ES ? MAXK_STREAM_AUX : 0);
+                        : sel_off(c[u]), 0, 0);
         if (pending) {
 #pragma unroll
             for (int u = 0; u < U; ++u)
@@ -293,8 +293,7 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int j = lane + kWave * i;
-            g[i] = MAXK_GROW_NT ? __builtin_nontemporal_load(&gr[j < D ? j : D - 1])
-                                : gr[j < D ? j : D - 1];
+            g[i] = gr[j < D ? j : D - 1];
         }
     };
     float gn[4];
@@ -665,16 +664,13 @@ __global__ __launch_bounds__(kBsortThreads) void bsort_push_kernel(
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int o = (base + u * G + grp) * 4;
-                a.w[u] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(vrs, o, 0, MAXK_STREAM_AUX));
-                a.r[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(rrs, o, 0, MAXK_STREAM_AUX);
+                a.w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, o, 0, 0));
+                a.r[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(rrs, o, 0, 0);
                 if (ES) {
                     a.s[u] = __builtin_amdgcn_raw_buffer_load_b32(
-                        srs, (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel), 0,
-                        MAXK_STREAM_AUX);
+                        srs, (int)((uint32_t)(base + u * G + grp) * (uint32_t)k + qsel), 0, 0);
                 } else {
-                    const uint32_t c =
-                        __builtin_amdgcn_raw_buffer_load_b32(crs, o, 0, MAXK_STREAM_AUX);
+                    const uint32_t c = __builtin_amdgcn_raw_buffer_load_b32(crs, o, 0, 0);
                     a.s[u] = __builtin_amdgcn_raw_buffer_load_b32(srs, (int)(c * (uint32_t)k + qsel),
                                                                   0, 0);
                 }
