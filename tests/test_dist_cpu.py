@@ -159,6 +159,24 @@ def test_sharded_matches_single_process(world, use_div, bounds, mode, pipeline):
     assert covered == V
 
 
+@pytest.mark.parametrize("mode,pipeline", [("gather", 1), ("gather", 2), ("halo", 1)])
+def test_sharded_matches_single_process_world8(mode, pipeline):
+    """The driver's scaling run goes to 8 ranks: the same check at world 8 (one rank per
+    process, gloo), with the pipelined exchange and the halo mode."""
+    V, D, k, seed = 600, 32, 8, 11
+    outs = _run(8, V, D, k, seed, True, None, mode, pipeline)
+    y_ref, gs_ref = _single(V, D, k, seed, True)
+    covered = 0
+    for rank, v0, v1, y, gs, bounds, xb, n_cols in outs:
+        if pipeline == 1:
+            np.testing.assert_array_equal(y, y_ref[v0:v1])
+        else:
+            np.testing.assert_allclose(y, y_ref[v0:v1], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(gs, gs_ref[v0:v1], rtol=1e-5, atol=BWD_ATOL)
+        covered += v1 - v0
+    assert covered == V
+
+
 def test_balanced_bounds_properties():
     row_ptr, _, _ = make_graph(1000, 5, 3)
     rp = torch.from_numpy(row_ptr)
