@@ -335,7 +335,7 @@ def main():
                          "maxk_dist's rule -- 2 when a rank's exchange is >= 64 MiB, else 1)")
     ap.add_argument("--edge-sel", default=None, choices=["auto", "0", "1"],
                     help="the forward's per-edge selector stream for a csc / bsort backward "
-                         "(MAXK_EDGE_SEL: auto = k <= 32, 0 never, 1 always)")
+                         "(MAXK_EDGE_SEL: auto = k <= 16, 0 never, 1 always)")
     ap.add_argument("--dist-mode", default="auto", choices=["auto", "gather", "halo"],
                     help="N > 1: all-gather every CBSR row, or exchange only the halo rows "
                          "(auto: halo when every shard's halo is at most 60 %% of the vertices)")
@@ -497,7 +497,7 @@ def main():
     pipelined = world > 1 and shard.pipeline > 1
     # csc / bsort backward: the forward writes each edge's selectors, phase 1 reads them in
     # order (maxk_spgemm_forward_sel / maxk_sspmm_backward_csc_sel / _bsort) where that pays:
-    # k <= 32 by default, MAXK_EDGE_SEL=0/1 off / on (mk.edge_selectors_wanted)
+    # k <= 16 by default, MAXK_EDGE_SEL=0/1 off / on (mk.edge_selectors_wanted)
     es = (torch.empty(El, k, dtype=torch.uint8, device=dev)
           if (not pipelined and args.bwd_mode in ("csc", "bsort") and El > 0
               and mk.edge_selectors_wanted(k)) else None)

@@ -857,18 +857,18 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     return out
 
 
-EDGE_SEL_KMAX = 32
+EDGE_SEL_KMAX = 16
 
 
 def edge_selectors_wanted(k: int) -> bool:
     """The rule for the per-edge selector stream given a csc / bsort backward: k % 4 == 0 and
     k <= EDGE_SEL_KMAX by default (MAXK_EDGE_SEL=auto); MAXK_EDGE_SEL=0 never, =1 at every
     k % 4 == 0.  Measured on the ogbn-products-sized graph: the forward that
-    writes the stream takes +0.68 / +0.80 / +0.83 ms at k = 8 / 16 / 32, the csc backward that
-    reads it -1.16 / -1.08 / -1.49 ms; at k = 32 the bench step gains 5 % (r04: 13.54 -> 12.88
-    ms; r03 2 %) and the 3-layer training epoch is unchanged (100.9 vs 101.1 ms, two runs each;
-    r03 -0.5 %), for num_e * k bytes (4 GB) held per layer from the forward to the backward.
-    None at 64 (+2.15 / -1.33 ms)."""
+    writes the stream takes +0.68 / +0.80 / +0.79 ms at k = 8 / 16 / 32, the csc backward that
+    reads it -1.16 / -1.08 / -0.93 ms.  At k = 32 that nets +1 % on the bench step and -1.5 % on
+    the 3-layer training epoch (r04, one box, alternating runs: 13.46 -> 13.31 ms, 100.1 ->
+    101.6 ms; profiles/r04/tune/es32/), for num_e * k bytes (4 GB) held per layer from the
+    forward to the backward, so the default stops at 16; none at 64 (+2.15 / -1.33 ms)."""
     mode = os.environ.get("MAXK_EDGE_SEL", "auto")
     if k % 4 or mode == "0":
         return False

@@ -253,11 +253,11 @@ def test_pull_slice_rule():
 
 def test_edge_selector_rule(monkeypatch):
     """The forward writes the per-edge selector stream for a csc / bsort backward where it
-    measured a net gain (k % 4 == 0, k <= 32); MAXK_EDGE_SEL=0 / 1 force it off / on."""
+    measured a net gain (k % 4 == 0, k <= 16); MAXK_EDGE_SEL=0 / 1 force it off / on."""
     import maxk_cuda_kernels as mk
     monkeypatch.delenv("MAXK_EDGE_SEL", raising=False)
     assert [mk.edge_selectors_wanted(k) for k in (4, 8, 12, 16, 32, 64, 10)] == \
-        [True, True, True, True, True, False, False]
+        [True, True, True, True, False, False, False]
     monkeypatch.setenv("MAXK_EDGE_SEL", "1")
     assert mk.edge_selectors_wanted(64) and not mk.edge_selectors_wanted(10)
     monkeypatch.setenv("MAXK_EDGE_SEL", "0")

@@ -37,7 +37,7 @@ TAIL_FIXTURE = os.path.join(GOLDEN, "topk", "topk_tail_overflow.npz")
 CONFIGS = [("reddit", 256, 8, "auto", "pull"), ("reddit", 256, 16, "auto", "pull"),
            ("reddit", 256, 32, "auto", "pull"), ("reddit", 256, 64, "auto", "pull"),
            ("products", 256, 8, "stream", "bsort"), ("products", 256, 16, "stream", "csc"),
-           ("products", 256, 32, "stream", "csc"), ("products", 256, 64, "auto", "csc"),
+           ("products", 256, 32, "auto", "csc"), ("products", 256, 64, "auto", "csc"),
            ("products_comm_ordered", 256, 32, "auto", "hybrid"),
            ("proteins", 256, 64, "auto", "pull"), ("flickr", 64, 16, "auto", "pull")]
 _GRAPHS = {}
