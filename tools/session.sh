@@ -19,6 +19,17 @@
 #             $CFGS; per-kernel averages in gpurun_out/<round>/pmc_set/<name>.txt
 #   statscfg  rocprofv3 --kernel-trace --stats of the configurations in $CFGS (as pmccfg);
 #             summaries in gpurun_out/<round>/stats_cfg/<name>.txt
+#   topkab    top-k GPU tests, then tools/topk_ab.py alternating the product library and the
+#             variants in $VARS (lib/variants/<name>, tools/tune.sh), two repeats
+#   ab        tools/ab_bench.sh over the variants in $VARS and the bench argument strings in
+#             $ABCFGS (separated by ';'); $R repeats
+#   window    the products forward with its columns folded into cache-sized windows
+#             (tools/fwd_slice_probe.py, k = 8 and 16)
+#   rehearse  N-rank rehearsals of the multi-GPU bench on the one GPU (gloo-staged
+#             collectives): Reddit k = 16 at N = 8 and 4, products k = 32 at N = 8; each run
+#             checks itself against the unsharded result (extra.dist_check_*)
+#   esab      products k = 32 with and without the edge-selector stream, alternating on one
+#             box: the bench line (3 repeats) and the 3-layer epoch (2 repeats)
 #   kt        the reference's kernel test (maxk_kernel_test.py) on every config graph, k = 8..64
 #   epochs    3-layer MaxK-SAGE epochs against the rocSPARSE model
 #   collect   (here, not on the box) copy gpurun_out/<round> into profiles/<round> and write
@@ -139,6 +150,68 @@ step_pmcset() {
 step_statscfg() {
   mkdir -p $O/stats_cfg
   cfg_loop stats_one
+}
+step_topkab() {
+  mkdir -p $O/topk
+  timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py -k topk -x -q --timeout 120 \
+    --timeout-method thread > $O/topk/pytest_topk.log 2>&1
+  tail -1 $O/topk/pytest_topk.log
+  local rep v lib rows
+  for rep in 1 2; do for v in base ${VARS:?VARS=\"variant ...\"}; do
+    lib=spgemm-prunning_amd/lib/variants/$v/libmaxk_hip.so
+    [ $v = base ] && lib=spgemm-prunning_amd/lib/libmaxk_hip.so
+    for rows in 232965 2449029; do
+      echo "== $v rows=$rows rep=$rep"
+      MAXK_HIP_LIB=$lib timeout -k 10 120 python tools/topk_ab.py --rows $rows
+    done
+  done; done > $O/topk/topk_ab.txt 2>&1
+}
+step_ab() {
+  mkdir -p $O/ab
+  local cfgs=()
+  IFS=';' read -ra cfgs <<< "${ABCFGS:?ABCFGS=\"--k 16;--graph products --k 8\"}"
+  timeout -k 10 900 bash tools/ab_bench.sh "base ${VARS:?}" "${cfgs[@]}" > $O/ab/ab.txt 2>&1
+  cat $O/ab/ab.txt
+}
+step_window() {
+  mkdir -p $O/probe
+  local k
+  for k in 8 16; do
+    timeout -k 10 300 python tools/fwd_slice_probe.py --graph products --k $k \
+      > $O/probe/fwd_window_products_k$k.txt 2>&1
+  done
+}
+rehearse_one() {  # rehearse_one <name> <ranks> <bench args...>
+  local n=$1 w=$2; shift 2
+  MAXK_DIST_BACKEND=gloo timeout -k 10 420 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node $w --master-addr 127.0.0.1 --master-port $((29500 + w)) bench.py \
+    --gpus $w --steps 5 --warmup 2 "$@" > $O/rehearsal/$n.json 2> $O/rehearsal/$n.err
+  python - $O/rehearsal/$n.json $n <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); e = d["extra"]
+print(sys.argv[2], "fwd err", e["dist_check_fwd_max_rel_err"], "bwd err",
+      e["dist_check_bwd_max_rel_err"], "mode", e["dist_mode"], "parts", e["dist_pipeline"],
+      "bwd", e["bwd_mode"], "stream", e["edge_sel_stream"], "ms/step", d["ms_per_step"])
+PY
+}
+step_rehearse() {
+  mkdir -p $O/rehearsal
+  rehearse_one n8_reddit 8
+  rehearse_one n4_reddit 4
+  rehearse_one n8_products_k32 8 --graph products
+}
+step_esab() {
+  mkdir -p $O/es32
+  local rep es
+  for rep in 1 2 3; do for es in 0 1; do
+    timeout -k 10 300 python bench.py --graph products --k 32 --edge-sel $es --steps 20 \
+      --no-cpu-baseline --no-rocsparse --no-cpu-spmm > $O/es32/bench_es${es}_$rep.json \
+      2> $O/es32/bench_es${es}_$rep.err
+  done; done
+  for rep in 1 2; do for es in 0 1; do
+    MAXK_EDGE_SEL=$es timeout -k 10 400 python3 spgemm-prunning_amd/maxk_train_bench.py \
+      products > $O/es32/epoch_es${es}_$rep.json 2> $O/es32/epoch_es${es}_$rep.err
+  done; done
 }
 step_kt() {
   mkdir -p $O/kernel_test
