@@ -51,11 +51,20 @@ inline int record_stride(int k, int64_t num_cols) {
     return (b + 127) / 128 * 128;
 }
 
-// Lanes per edge in the main kernel: pow2ceil(k), at least 8 (bounds the LDS
-// copies per wave to 8).
-inline int fwd_lanes_per_edge(int k) {
+// Lanes per edge in the main kernel: pow2ceil(k), at least 8 (bounds the LDS copies per wave
+// to 8, one per edge group).  On a sparse graph (average degree below kFwdSparseDegree) at
+// least 16: a wave then walks many short rows, one dependent round of loads and an LDS flush
+// each, and its 8 LDS copies at 8 lanes per edge (8.3 KB per wave at D = 256) cap a CU at 16
+// waves; 16 lanes per edge (half of them idle at k <= 8) halve the copies and lift the cap to
+// the VGPR limit (28 waves).  ogbn-products-sized, k = 8, forward with the edge-selector
+// stream: 3.44 -> 3.16 ms, and 3.37 -> 3.15 ms on another box; Reddit-sized (average degree
+// 492), where rows are long and the doubled gather instructions cost more than the occupancy
+// buys: 1.395 -> 1.44 ms, so it keeps 8 (profiles/r04/tune/fwd_occupancy_ab*.txt).
+constexpr int64_t kFwdSparseDegree = 128;
+inline int fwd_lanes_per_edge(int k, int64_t num_rows, int64_t num_e) {
     const int g = lanes_per_edge(k);
-    return g < 8 ? 8 : g;
+    const int gmin = num_e < kFwdSparseDegree * num_rows ? 16 : 8;
+    return g < gmin ? gmin : g;
 }
 
 // Packs the records of groups of whole vertices (vpw = min(32, 512 / k) per
@@ -564,7 +573,7 @@ FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, i
     L.n_items = (int)(n > 0 ? n : 1);
     L.RS = record_stride(k, num_cols);
     L.DS = copy_stride(D);
-    L.kg = fwd_lanes_per_edge(k);
+    L.kg = fwd_lanes_per_edge(k, num_rows, num_e);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     L.rec_off = 0;
     L.rec_bytes = al((size_t)num_cols * L.RS);
