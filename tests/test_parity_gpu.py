@@ -55,6 +55,35 @@ def test_topk_bit_exact(mk, cuda, path):
     assert np.array_equal(v.cpu().numpy(), z["topk_val"])
 
 
+@pytest.mark.parametrize("k", [2, 4, 8])
+@pytest.mark.parametrize("D,chunk", [(256, 0), (256, 97), (64, 0)])
+def test_forward_dense_small_k(mk, cuda, k, D, chunk):
+    """The forward's lane rule (fwd_lanes_per_edge): at k <= 8 a graph with an average degree
+    of at least 128 takes 8 lanes per edge, a sparser one 16.  The golden graphs are sparse,
+    so this dense one (average degree ~170, one hub row split over items at chunk 97) covers
+    the 8-lane kernels -- plain, with the degree division, and writing the edge-selector
+    stream -- against the oracle."""
+    rng = np.random.default_rng(1000 + k + D)
+    V = 900
+    deg = rng.integers(120, 220, V)
+    deg[7] = V - 1  # a hub row
+    rp = np.zeros(V + 1, np.int32)
+    rp[1:] = np.cumsum(deg)
+    E = int(rp[-1])
+    assert E >= 128 * V
+    col = np.concatenate([np.sort(rng.choice(V, int(d), replace=False)) for d in deg]).astype(np.int32)
+    val = rng.random(E, dtype=np.float32)
+    x = rng.standard_normal((V, D)).astype(np.float32)
+    tv, ti = O.topk(x, k)
+    div = np.maximum(deg, 1).astype(np.float32)
+    ref = O.spgemm_fwd(rp, col, val, tv, ti, D, row_div=div)
+    args = (T(rp, cuda), T(col, cuda), T(val, cuda), T(tv, cuda), T(ti, cuda), D)
+    close(mk.spgemm_forward(*args, row_div=T(div, cuda), chunk=chunk), ref)
+    es = torch.empty(E, k, dtype=torch.uint8, device=cuda)
+    close(mk.spgemm_forward(*args, row_div=T(div, cuda), chunk=chunk, edge_sel_out=es), ref)
+    assert torch.equal(es, T(ti, cuda)[T(col, cuda).long()])
+
+
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_forward_golden(mk, cuda, path, chunk):
