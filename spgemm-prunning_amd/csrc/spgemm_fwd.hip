@@ -563,6 +563,7 @@ inline int copy_stride(int D) { return ((D + 3) / 4) * 4 + 4; }
 
 struct FwdLayout {
     int chunk, n_items, RS, DS, kg;
+    bool deep;  // dense graph (average degree >= kFwdSparseDegree): deeper load batches
     size_t rec_off, rec_bytes, slab_off, slab_bytes, row_off, total;
 };
 
@@ -574,6 +575,7 @@ FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, i
     L.RS = record_stride(k, num_cols);
     L.DS = copy_stride(D);
     L.kg = fwd_lanes_per_edge(k, num_rows, num_e);
+    L.deep = num_e >= kFwdSparseDegree * num_rows;
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     L.rec_off = 0;
     L.rec_bytes = al((size_t)num_cols * L.RS);
@@ -601,6 +603,14 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, true>), grid, dim3(kBlock), lds, s,
                            row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
                            num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, esel);
+    else if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32) && L.deep)
+        // dense graphs: 16 wave steps of loads per batch (Reddit-sized k = 16 forward 1.613 ->
+        // 1.594 ms, k = 32 / 64 and ogbn-proteins 0.3-0.8 % faster; on the sparse products
+        // graph, whose rows hold ~50 edges, 16 steps cost occupancy for nothing: 3.23 -> 4.19
+        // ms at k = 8; profiles/r04/tune/fwd_batch_depth_ab*.txt)
+        hipLaunchKernelGGL((spgemm_fwd_kernel<KG, 2 * U, false, false>), grid, dim3(kBlock), lds,
+                           s, row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
+                           num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, nullptr);
     else if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32))
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, false>), grid, dim3(kBlock), lds, s,
                            row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,

@@ -55,14 +55,14 @@ def test_topk_bit_exact(mk, cuda, path):
     assert np.array_equal(v.cpu().numpy(), z["topk_val"])
 
 
-@pytest.mark.parametrize("k", [2, 4, 8])
+@pytest.mark.parametrize("k", [2, 4, 8, 16, 32])
 @pytest.mark.parametrize("D,chunk", [(256, 0), (256, 97), (64, 0)])
 def test_forward_dense_small_k(mk, cuda, k, D, chunk):
-    """The forward's lane rule (fwd_lanes_per_edge): at k <= 8 a graph with an average degree
-    of at least 128 takes 8 lanes per edge, a sparser one 16.  The golden graphs are sparse,
-    so this dense one (average degree ~170, one hub row split over items at chunk 97) covers
-    the 8-lane kernels -- plain, with the degree division, and writing the edge-selector
-    stream -- against the oracle."""
+    """The forward's dense-graph rules (average degree >= 128): 8 lanes per edge at k <= 8
+    (fwd_lanes_per_edge; a sparser graph takes 16) and 16 wave steps of loads per batch
+    (FwdLayout::deep).  The golden graphs are sparse, so this dense one (average degree ~170,
+    one hub row split over items at chunk 97) covers those kernels -- plain, with the degree
+    division, and the stream-writing one (which keeps 8 steps) -- against the oracle."""
     rng = np.random.default_rng(1000 + k + D)
     V = 900
     deg = rng.integers(120, 220, V)
