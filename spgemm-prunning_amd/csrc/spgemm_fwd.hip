@@ -471,12 +471,18 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
     int r = wave_first_row_token(row_ptr, num_rows, d0);
 
     // Continuation of row r-1 (its token precedes d0): edges e with e + r in [d0, d1).
+    // A row of at most `chunk` edges is never split: the item holding its row token walks all
+    // of it, past d1, so only longer (hub) rows leave a continuation and a slab for the fixup
+    // (Reddit-sized k = 16 forward 1.596 -> 1.585 ms, ogbn-products-sized k = 8 3.237 -> 3.19
+    // ms, proteins unchanged; profiles/r04/tune/fwd_snap_rows_ab.txt).  An item then walks at
+    // most 2 * chunk tokens.
     int cont = -1;
     if (r > 0) {
         const int64_t sb = d0 - r;
         int64_t se = (int64_t)row_ptr[r];
         if (d1 - r < se) se = d1 - r;
-        if (sb < se) {
+        const bool whole = (int64_t)row_ptr[r] - row_ptr[r - 1] <= chunk;
+        if (sb < se && !whole) {
             wave_lds_fence();
             EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se,
                                                k, DS - 1, lane, esel);
@@ -536,7 +542,7 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
             }
         }
         int64_t se = (int64_t)row_ptr[r + 1];
-        if (d1 - r - 1 < se) se = d1 - r - 1;
+        if (d1 - r - 1 < se && se - rb > chunk) se = d1 - r - 1;  // a hub row: split
         wave_lds_fence();
         if (rb < se)
             EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se,
