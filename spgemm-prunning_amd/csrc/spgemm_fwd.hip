@@ -554,13 +554,30 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
     }
 }
 
-int fwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk) {
+// Waves of the plain forward one CU holds at once: 7 per SIMD by VGPRs (65-69 VGPRs, the
+// kernel-resource-usage remarks), 4 for the deep-batch kernel (~100), fewer when the LDS copies
+// (NC rows of DS floats per wave) fill the CU's 160 KB first.
+int fwd_resident_waves(int kg, int DS, bool deep) {
+    const int by_vgpr = deep ? 4 * 4 : 7 * 4;
+    const size_t per_block = (size_t)kWavesPerBlock * (kWave / kg) * DS * sizeof(float);
+    const int by_lds = (int)(kPullLdsBytes / per_block) * kWavesPerBlock;
+    return by_lds < by_vgpr ? by_lds : by_vgpr;
+}
+
+int fwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int resident) {
     if (chunk > 0) return chunk;
     // ~8 waves of work per resident wave slot on 256 CUs, within [256, 2048] tokens
     const int64_t total = num_rows + num_e;
     int64_t c = ceil_div(total, 256LL * 32 * 8);
-    c = c < 256 ? 256 : (c > 2048 ? 2048 : c);
-    return (int)c;
+    if (c >= 256) return (int)(c > 2048 ? 2048 : c);
+    // A smaller graph has fewer items than wave slots at 256 tokens: size the items so all of
+    // them are resident in one round (90 % of the slots, for uneven block placement), since each
+    // wave is a chain of dependent gathers and a second round costs a whole item's latency.
+    // Flickr-sized (1.08M tokens, 7168 slots): 151 tokens would fill every slot; the forward at
+    // 144 / 160 / 176 / 192 / 256 tokens takes 0.0527 / 0.049 / 0.051 / 0.053 / 0.0585 ms
+    // (profiles/r04/tune/flickr_chunk_sweep.txt).
+    c = ceil_div(total * 10, 256LL * resident * 9);
+    return (int)(c < 64 ? 64 : (c > 256 ? 256 : c));
 }
 
 // LDS row stride per copy: D padded to 16 B, plus one 16-B group holding the
@@ -575,13 +592,13 @@ struct FwdLayout {
 
 FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, int k, int chunk) {
     FwdLayout L{};
-    L.chunk = fwd_chunk(num_rows, num_e, chunk);
-    const int64_t n = ceil_div(num_rows + num_e, L.chunk);
-    L.n_items = (int)(n > 0 ? n : 1);
     L.RS = record_stride(k, num_cols);
     L.DS = copy_stride(D);
     L.kg = fwd_lanes_per_edge(k, num_rows, num_e);
     L.deep = num_e >= kFwdSparseDegree * num_rows;
+    L.chunk = fwd_chunk(num_rows, num_e, chunk, fwd_resident_waves(L.kg, L.DS, L.deep));
+    const int64_t n = ceil_div(num_rows + num_e, L.chunk);
+    L.n_items = (int)(n > 0 ? n : 1);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     L.rec_off = 0;
     L.rec_bytes = al((size_t)num_cols * L.RS);
