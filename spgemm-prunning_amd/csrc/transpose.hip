@@ -415,6 +415,26 @@ extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t di
     int64_t s = (num_rows * dim_origin * 4 + per - 1) / per;
     const int64_t lo = (num_rows + 65535) / 65536;  // rows within a slice fit 16 bits
     s = s < lo ? lo : s;
+    // A small graph's pull is a few rounds of workgroups, one per CU (a part's slot table
+    // fills the LDS), so a nearly empty last round costs a whole round: of the slice counts
+    // in [ceil(s/2), s], take the largest with the fewest rounds when s makes at most 5
+    // (num_cols taken as num_rows).  Flickr-sized (89k rows, D = 64; 220 / 264 / 704 / 1056
+    // workgroups at k = 8 / 16 / 32 / 64): k = 16 S = 3 -> 2, 0.054 -> 0.046 ms; k = 32 4 -> 2,
+    // 0.069 -> 0.064; k = 64 3 -> 2, 0.111 -> 0.100; k = 8 keeps 5 (0.037)
+    // (profiles/r04/tune/flickr_pull_slices.txt).  Reddit- and proteins-sized graphs make
+    // 1.6k-15k workgroups and keep the rule above.
+    if (dim_k % 4 == 0 && MAXK_PULL_Q) {
+        const int shift = maxk_pull_shift(dim_k);
+        const int64_t wg = maxk_bucket_count(num_rows, shift) * parts;  // per slice
+        const int64_t cus = 256;
+        auto rounds = [&](int64_t n) { return (n * wg + cus - 1) / cus; };
+        if (shift > 0 && wg > 0 && rounds(s) <= 5) {
+            int64_t best = s;
+            for (int64_t c = s - 1; c >= (s + 1) / 2 && c >= lo; --c)
+                if (rounds(c) < rounds(best)) best = c;
+            s = best;
+        }
+    }
     return (int)(s < 1 ? 1 : (s > 256 ? 256 : s));
 }
 

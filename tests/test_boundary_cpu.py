@@ -244,6 +244,9 @@ def test_pull_slice_rule():
     assert L.maxk_pull_slices(100_000_000, 256, 16) == 256
     assert L.maxk_pull_slices(2_449_029, 256, 64) == 228
     assert L.maxk_pull_slices(4_000_000, 16, 64) == 62  # rows in a slice stay <= 65536
+    # Flickr-sized (89k rows, D = 64): 132 / 352 / 264 tiles at k = 16 / 32 / 64 would leave
+    # a nearly empty last round of workgroups; the slices drop to 2 (k = 8 keeps 5: 220, one round)
+    assert [L.maxk_pull_slices(89250, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
     gp = (232965 * 256 * 4 + 255) // 256 * 256
     selq = 2 * ((232965 * 16 + 255) // 256 * 256)  # slot-ordered selectors + their l map
     assert L.maxk_sspmm_backward_pull_workspace_size(232965, 232965, 256, 16, 65) == \
