@@ -483,10 +483,10 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         if (d1 - r < se) se = d1 - r;
         const bool whole = (int64_t)row_ptr[r] - row_ptr[r - 1] <= chunk;
         if (sb < se && !whole) {
+            const float div = row_div ? row_div[r - 1] : 1.f;  // loaded before the walk
             wave_lds_fence();
             EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se,
                                                k, DS - 1, lane, esel);
-            const float div = row_div ? row_div[r - 1] : 1.f;
             flush_row<NC>(acc, DS, slab + (int64_t)item * D, D, div, row_div != nullptr, lane);
             cont = r - 1;
         }
@@ -528,12 +528,15 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
                     const int lj = __shfl(rpn, j) - __shfl(rpj, j);
                     maxlen = lj > maxlen ? lj : maxlen;
                 }
+                // the batch's divisors, one per lane, loaded before the walk (not one
+                // dependent scalar load per row after it)
+                const float divq = row_div && lane < m ? row_div[r + lane] : 1.f;
                 wave_lds_fence();
                 EdgeWalker<KG, U, WIDE, EMIT>::run_rows(acc_g, col_idx, edge_val, rec, RS, e0,
                                                         e_end, sb_g, len_g, (maxlen + U - 1) / U,
                                                         k, DS - 1, lane, esel);
                 for (int j = 0; j < m; ++j) {
-                    const float div = row_div ? row_div[r + j] : 1.f;
+                    const float div = __shfl(divq, j);
                     flush_row<1>(acc + j * DS, DS, out + (int64_t)(r + j) * D, D, div,
                                  row_div != nullptr, lane, accumulate & 1, accumulate & 2);
                 }
@@ -543,11 +546,11 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         }
         int64_t se = (int64_t)row_ptr[r + 1];
         if (d1 - r - 1 < se && se - rb > chunk) se = d1 - r - 1;  // a hub row: split
+        const float div = row_div ? row_div[r] : 1.f;  // loaded before the walk
         wave_lds_fence();
         if (rb < se)
             EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se,
                                                k, DS - 1, lane, esel);
-        const float div = row_div ? row_div[r] : 1.f;
         flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane,
                       accumulate & 1, accumulate & 2);
         ++r;
