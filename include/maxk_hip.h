@@ -63,7 +63,9 @@ const char *maxk_build_config(void);
  *           its launcher spmm_kernel_opt2_sparse_v3_wrapper
  *           (cuda_kernel_wrappers.cu:38-56) and the /in_degrees of
  *           maxk_spgemm_function.py:85-86.
- * chunk_edges: edges per wavefront work item (0 = auto).
+ * chunk_edges: tokens (rows + edges) per wavefront work item (0 = auto: about 8 items per
+ *              resident wave slot in [256, 2048], or on a smaller graph all items resident
+ *              in one round, down to 64).
  * workspace: >= maxk_spgemm_forward_workspace_size(...) bytes, 256-B aligned
  *            (packed CBSR records + split-row slabs).
  * ------------------------------------------------------------------------- */
@@ -308,7 +310,8 @@ int maxk_sspmm_backward_pull_tiles(const float *grad_out, const float *row_div,
  * (the backward's 16-B selector copies need 16 | 2^shift * k).  maxk_pull_shift(k) is the
  * bucket shift to use (at least 4); maxk_pull_slices(num_rows, dim_origin, dim_k) the default
  * slice count (about 3.5 MiB of G rows per slice and rank part of k -- at most 3 parts' worth
- * -- at least num_rows/65536, 1..256). */
+ * -- at least num_rows/65536, 1..256; when that makes at most 5 rounds of workgroups, one per
+ * CU, the count in [ceil(S/2), S] with the fewest rounds). */
 int maxk_pull_shift(int32_t dim_k);
 int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
