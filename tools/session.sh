@@ -28,6 +28,7 @@
 #   rehearse  N-rank rehearsals of the multi-GPU bench on the one GPU (gloo-staged
 #             collectives): Reddit k = 16 at N = 8 and 4, products k = 32 at N = 8; each run
 #             checks itself against the unsharded result (extra.dist_check_*)
+#   rehearsek8  the same for products k = 8 at N = 8 (bsort backward, edge-selector stream)
 #   esab      products k = 32 with and without the edge-selector stream, alternating on one
 #             box: the bench line (3 repeats) and the 3-layer epoch (2 repeats)
 #   kt        the reference's kernel test (maxk_kernel_test.py) on every config graph, k = 8..64
@@ -199,6 +200,10 @@ step_rehearse() {
   rehearse_one n8_reddit 8
   rehearse_one n4_reddit 4
   rehearse_one n8_products_k32 8 --graph products
+}
+step_rehearsek8() {  # products k = 8 at N = 8: the sharded bsort backward and selector stream
+  mkdir -p $O/rehearsal
+  rehearse_one n8_products_k8 8 --graph products --k 8
 }
 step_esab() {
   mkdir -p $O/es32
