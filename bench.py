@@ -12,10 +12,14 @@ self loops), hidden D=256, k=16 -- BASELINE.json configs[1] at k=16.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--graph reddit] [--k 16]
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): vertex-range
-shards balanced by nnz; per step an RCCL all-gather of the CBSR rows before the
-forward and a reduce-scatter of the CBSR-gradient partials after the backward
-(strong scaling: the graph is fixed).  Rank 0 prints ONE JSON line.
+N > 1, one rank per GPU: vertex-range shards balanced by nnz; per step an RCCL
+all-gather of the CBSR rows before the forward and a reduce-scatter of the
+CBSR-gradient partials after the backward (strong scaling: the graph is fixed).
+Rank 0 prints ONE JSON line.  Launched either by torch.distributed.run
+(WORLD_SIZE set: this process is one rank) or directly -- `python bench.py
+--gpus N` with no WORLD_SIZE starts N ranks itself (launch_ranks: a child
+torch.distributed.run on 127.0.0.1, before this process touches the GPU) and
+exits with their status.
 """
 from __future__ import annotations
 
@@ -308,6 +312,32 @@ def cpu_spmm_baselines(row_ptr, col, val, dense, target_s=6.0):
     return out
 
 
+# --------------------------------------------------------------------------- launcher
+def launch_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` without torch.distributed.run: start the
+    N ranks as one child `python -m torch.distributed.run` on 127.0.0.1 and return its exit
+    status.  This process only parses arguments and counts devices (torch.cuda.device_count()
+    does not initialise HIP on this image): it makes no HIP call and never execs, so the ranks
+    are fresh processes.  Rank 0's JSON line reaches the shared stdout unchanged.  With fewer
+    visible GPUs than ranks the collectives are staged through the host (MAXK_DIST_BACKEND=gloo,
+    the one-GPU rehearsal) unless the caller chose a backend."""
+    import socket
+    import subprocess
+    env = dict(os.environ)
+    ndev = torch.cuda.device_count()
+    if ndev < n and "MAXK_DIST_BACKEND" not in env:
+        env["MAXK_DIST_BACKEND"] = "gloo"
+        log(f"[bench] {n} ranks on {ndev} visible GPU(s): gloo-staged collectives")
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *argv]
+    log(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=env)
+
+
 # --------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -340,6 +370,8 @@ def main():
                     help="N > 1: all-gather every CBSR row, or exchange only the halo rows "
                          "(auto: halo when every shard's halo is at most 60 %% of the vertices)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     if args.edge_sel is not None:
         os.environ["MAXK_EDGE_SEL"] = args.edge_sel
 

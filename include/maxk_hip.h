@@ -158,6 +158,9 @@ int maxk_sspmm_backward_csc_sel(const int32_t *row_ptr, const int32_t *col_idx,
  * so a stream that works on a small graph works on a large one. */
 int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_idx, int64_t num_e,
                         int32_t dim_k, uint8_t *edge_sel, void *stream);
+/* Workgroups (256 threads) maxk_edge_selectors launches for n_words words: capped at 64 per
+ * CU and walked grid-stride, so num_e * k one-byte words past 2^32 still launch. */
+int64_t maxk_edge_selectors_blocks(int64_t n_words);
 
 /* Transpose plan of a CSR graph (once per graph): col_ptr[num_cols+1] of the
  * CSC and csc_eid[num_e] = the CSR edge id held by CSC slot t (stable in CSR order).
@@ -308,12 +311,14 @@ int maxk_sspmm_backward_pull_tiles(const float *grad_out, const float *row_div,
  * in CSR order, ent[2*num_e] = one uint32 pair per edge: {row - first row of its slice |
  * (column - first column of its bucket) << 16, bits of edge_val}; bucket_shift in [4, 15]
  * (the backward's 16-B selector copies need 16 | 2^shift * k).  maxk_pull_shift(k) is the
- * bucket shift to use (at least 4); maxk_pull_slices(num_rows, dim_origin, dim_k) the default
+ * bucket shift to use (at least 4); maxk_pull_slices(num_rows, num_cols, dim_origin, dim_k) the
+ * default
  * slice count (about 3.5 MiB of G rows per slice and rank part of k -- at most 3 parts' worth
  * -- at least num_rows/65536, 1..256; when that makes at most 5 rounds of workgroups, one per
- * CU, the count in [ceil(S/2), S] with the fewest rounds). */
+ * CU of the current device, over num_cols' buckets, the count in [ceil(S/2), S] with the
+ * fewest rounds; num_cols <= 0 means num_rows). */
 int maxk_pull_shift(int32_t dim_k);
-int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k);
+int maxk_pull_slices(int64_t num_rows, int64_t num_cols, int32_t dim_origin, int32_t dim_k);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
                                      int32_t bucket_shift, int32_t slices);
 int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
@@ -414,10 +419,11 @@ int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_val, uint8_t
 /* Rows (over every top-k launch on the current device since the last reset) whose threshold
  * search took other than dim_k winners -- a kernel bug, never expected.  The kernels count such
  * rows, and such a row never writes past its own k winner slots (r02's fault: a dead row's
- * extra winners overwrote another wave's); its own output row is then undefined.  Synchronous
- * (waits for the device); reset != 0 zeroes
- * the count.  The Python binding checks it after every top-k under MAXK_VALIDATE=1. */
-int maxk_topk_error_rows(int64_t *rows, int32_t reset);
+ * extra winners overwrote another wave's); its own output row is then undefined.  Read (and,
+ * with reset != 0, zeroed) in order on `stream`, which it synchronises (not the device, so a
+ * hipGraph capture on another stream is left alone).  The Python binding zeroes it before
+ * and reads it after every top-k under MAXK_VALIDATE=1, so a count is the launch's own. */
+int maxk_topk_error_rows(int64_t *rows, int32_t reset, void *stream);
 
 /* dense[r,:] = 0; dense[r, cbsr_idx[r,l]] = cbsr_val[r,l]  (all of dense written).
  * Replaces: zeros(V,D).scatter_(1, sel, grad_sparse), maxk_spgemm_function.py:152,175. */

@@ -589,16 +589,22 @@ inline int copy_stride(int D) { return ((D + 3) / 4) * 4 + 4; }
 
 struct FwdLayout {
     int chunk, n_items, RS, DS, kg;
-    bool deep;  // dense graph (average degree >= kFwdSparseDegree): deeper load batches
+    // the deep-batch kernel runs: a dense graph (average degree >= kFwdSparseDegree), 32-bit
+    // record offsets, no selector stream written (launch_fwd)
+    bool deep;
     size_t rec_off, rec_bytes, slab_off, slab_bytes, row_off, total;
 };
 
-FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, int k, int chunk) {
+// emit: the launch writes the edge-selector stream (the U-step kernel, whatever the graph), so
+// small graphs' items are sized for that kernel's occupancy
+FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, int k, int chunk,
+                     bool emit = false) {
     FwdLayout L{};
     L.RS = record_stride(k, num_cols);
     L.DS = copy_stride(D);
     L.kg = fwd_lanes_per_edge(k, num_rows, num_e);
-    L.deep = num_e >= kFwdSparseDegree * num_rows;
+    L.deep = !emit && num_e >= kFwdSparseDegree * num_rows && num_cols < (1 << 24) &&
+             (uint64_t)num_cols * (uint64_t)L.RS < (1ull << 32);
     L.chunk = fwd_chunk(num_rows, num_e, chunk, fwd_resident_waves(L.kg, L.DS, L.deep));
     const int64_t n = ceil_div(num_rows + num_e, L.chunk);
     L.n_items = (int)(n > 0 ? n : 1);
@@ -629,7 +635,7 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, true>), grid, dim3(kBlock), lds, s,
                            row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
                            num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, esel);
-    else if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32) && L.deep)
+    else if (L.deep)
         // dense graphs: 16 wave steps of loads per batch (Reddit-sized k = 16 forward 1.613 ->
         // 1.594 ms, k = 32 / 64 and ogbn-proteins 0.3-0.8 % faster; on the sparse products
         // graph, whose rows hold ~50 edges, 16 steps cost occupancy for nothing: 3.23 -> 4.19
@@ -656,7 +662,11 @@ extern "C" size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t n
                                                      int64_t num_e, int32_t dim_origin,
                                                      int32_t dim_k, int32_t chunk_edges) {
     if (num_rows < 0 || num_cols < 0 || num_e < 0 || dim_origin <= 0 || dim_k <= 0) return 0;
-    return fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges).total;
+    // one workspace serves the plain and the stream-writing launch (their item sizes differ)
+    const size_t a = fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges).total;
+    const size_t b =
+        fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, true).total;
+    return a > b ? a : b;
 }
 
 namespace {
@@ -680,7 +690,8 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
     MAXK_REQUIRE(num_e == 0 || (col_idx && edge_val && cbsr_val && cbsr_idx),
                  "CSR/CBSR pointers must not be NULL");
     MAXK_REQUIRE(num_e == 0 || num_cols > 0, "edges present but num_cols == 0");
-    const FwdLayout L = fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges);
+    const FwdLayout L =
+        fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, esel != nullptr);
     MAXK_REQUIRE(workspace && workspace_bytes >= L.total,
                  "workspace too small: need %zu bytes, got %zu", L.total, workspace_bytes);
     MAXK_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-B aligned");

@@ -1617,18 +1617,23 @@ __global__ __launch_bounds__(kBlock) void edge_sel_kernel(const int32_t *__restr
                                                           const uint8_t *__restrict__ cbsr_idx,
                                                           uint8_t *__restrict__ edge_sel,
                                                           int64_t n_words, int k, int wb) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n_words) return;
+    // grid-stride: the launch caps its grid (num_e * k one-byte words can pass the
+    // 2^32 - 1 threads of one grid dimension)
     const int wpe = k / wb;  // words per edge
-    const int64_t e = i / wpe;
-    const int w = (int)(i % wpe);
-    const size_t src = (size_t)(uint32_t)col_idx[e] * k + (size_t)w * wb;
-    if (wb == 16)
-        reinterpret_cast<uint4 *>(edge_sel)[i] = *reinterpret_cast<const uint4 *>(cbsr_idx + src);
-    else if (wb == 4)
-        reinterpret_cast<uint32_t *>(edge_sel)[i] = *reinterpret_cast<const uint32_t *>(cbsr_idx + src);
-    else
-        edge_sel[i] = cbsr_idx[src];
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_words; i += stride) {
+        const int64_t e = i / wpe;
+        const int w = (int)(i % wpe);
+        const size_t src = (size_t)(uint32_t)col_idx[e] * k + (size_t)w * wb;
+        if (wb == 16)
+            reinterpret_cast<uint4 *>(edge_sel)[i] =
+                *reinterpret_cast<const uint4 *>(cbsr_idx + src);
+        else if (wb == 4)
+            reinterpret_cast<uint32_t *>(edge_sel)[i] =
+                *reinterpret_cast<const uint32_t *>(cbsr_idx + src);
+        else
+            edge_sel[i] = cbsr_idx[src];
+    }
 }
 }  // namespace
 }  // namespace maxk
@@ -1665,6 +1670,12 @@ extern "C" int maxk_sspmm_backward_csc_sel(const int32_t *row_ptr, const int32_t
                     workspace, workspace_bytes, stream);
 }
 
+// edge_sel_kernel's grid: one thread per word up to 64 workgroups per CU, then grid-stride
+extern "C" int64_t maxk_edge_selectors_blocks(int64_t n_words) {
+    const int64_t b = ceil_div(n_words < 0 ? 0 : n_words, (int64_t)kBlock);
+    return b < 256 * 64 ? b : 256 * 64;
+}
+
 extern "C" int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_idx,
                                    int64_t num_e, int32_t dim_k, uint8_t *edge_sel, void *stream) {
     clear_error();
@@ -1677,7 +1688,7 @@ extern "C" int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_i
     const uintptr_t al = (uintptr_t)edge_sel | (uintptr_t)cbsr_idx;
     const int wb = dim_k % 16 == 0 && (al & 15) == 0 ? 16 : dim_k % 4 == 0 && (al & 3) == 0 ? 4 : 1;
     const int64_t n_words = num_e * (dim_k / wb);
-    hipLaunchKernelGGL(edge_sel_kernel, dim3((unsigned)ceil_div(n_words, kBlock)), dim3(kBlock), 0,
+    hipLaunchKernelGGL(edge_sel_kernel, dim3((unsigned)maxk_edge_selectors_blocks(n_words)), dim3(kBlock), 0,
                        as_stream(stream), col_idx, cbsr_idx, edge_sel, n_words, dim_k, wb);
     MAXK_LAUNCHED("edge_sel_kernel");
     return MAXK_OK;

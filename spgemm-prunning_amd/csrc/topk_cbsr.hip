@@ -674,17 +674,19 @@ extern "C" int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_v
                                 dim_k, stream);
 }
 
-extern "C" int maxk_topk_error_rows(int64_t *rows, int32_t reset) {
+extern "C" int maxk_topk_error_rows(int64_t *rows, int32_t reset, void *stream) {
     clear_error();
     MAXK_REQUIRE(rows, "rows must not be NULL");
+    hipStream_t s = as_stream(stream);
     uint32_t v = 0;
-    MAXK_HIP(hipDeviceSynchronize());
-    MAXK_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_topk_bad_rows), sizeof(v), 0,
-                                 hipMemcpyDeviceToHost));
+    MAXK_HIP(hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_topk_bad_rows), sizeof(v), 0,
+                                      hipMemcpyDeviceToHost, s));
+    MAXK_HIP(hipStreamSynchronize(s));
     if (reset && v) {
-        const uint32_t z = 0;
-        MAXK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_topk_bad_rows), &z, sizeof(z), 0,
-                                   hipMemcpyHostToDevice));
+        static const uint32_t z = 0;
+        MAXK_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_topk_bad_rows), &z, sizeof(z), 0,
+                                        hipMemcpyHostToDevice, s));
+        MAXK_HIP(hipStreamSynchronize(s));
     }
     *rows = v;
     return MAXK_OK;

@@ -405,8 +405,22 @@ static int pull_parts_of(int32_t dim_k) {
 // a row's columns, the more rows a slice may hold -- k = 8 (one 8-slot part) best at
 // S = 44 (5.3 MiB; 1.400 ms against 1.418 at S = 66), k = 16 (two 8-slot parts) at S = 28
 // (4.1 MiB per part; 2.120 against 2.145 at S = 33), k = 32 (two 16-slot parts) still at 33.
-extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t dim_k) {
+// CUs of the current device (one pull workgroup per CU at a time); 256 (MI355X) without one
+static int64_t device_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0) {
+        (void)hipGetLastError();
+        return 256;
+    }
+    return n;
+}
+
+extern "C" int maxk_pull_slices(int64_t num_rows, int64_t num_cols, int32_t dim_origin,
+                                int32_t dim_k) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
+    if (num_cols <= 0) num_cols = num_rows;
     const int parts = dim_k % 4 == 0 ? pull_parts_of(dim_k) : 1;
     const int64_t part_bytes = dim_k <= 8    ? maxk::kPullSliceBytes * 3 / 2
                                : dim_k <= 16 ? maxk::kPullSliceBytes * 33 / 28
@@ -418,15 +432,15 @@ extern "C" int maxk_pull_slices(int64_t num_rows, int32_t dim_origin, int32_t di
     // A small graph's pull is a few rounds of workgroups, one per CU (a part's slot table
     // fills the LDS), so a nearly empty last round costs a whole round: of the slice counts
     // in [ceil(s/2), s], take the largest with the fewest rounds when s makes at most 5
-    // (num_cols taken as num_rows).  Flickr-sized (89k rows, D = 64; 220 / 264 / 704 / 1056
+    // (buckets counted over num_cols, rounds over the device's CUs: ADVICE r04).  Flickr-sized (89k rows, D = 64; 220 / 264 / 704 / 1056
     // workgroups at k = 8 / 16 / 32 / 64): k = 16 S = 3 -> 2, 0.054 -> 0.046 ms; k = 32 4 -> 2,
     // 0.069 -> 0.064; k = 64 3 -> 2, 0.111 -> 0.100; k = 8 keeps 5 (0.037)
     // (profiles/r04/tune/flickr_pull_slices.txt).  Reddit- and proteins-sized graphs make
     // 1.6k-15k workgroups and keep the rule above.
     if (dim_k % 4 == 0 && MAXK_PULL_Q) {
         const int shift = maxk_pull_shift(dim_k);
-        const int64_t wg = maxk_bucket_count(num_rows, shift) * parts;  // per slice
-        const int64_t cus = 256;
+        const int64_t wg = maxk_bucket_count(num_cols, shift) * parts;  // per slice
+        const int64_t cus = device_cus();
         auto rounds = [&](int64_t n) { return (n * wg + cus - 1) / cus; };
         if (shift > 0 && wg > 0 && rounds(s) <= 5) {
             int64_t best = s;

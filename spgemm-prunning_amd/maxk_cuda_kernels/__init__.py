@@ -73,6 +73,13 @@ def _validate_default() -> bool:
 _CHECKED: "dict" = {}
 
 
+def _ver(t):
+    """Version counter of a cached-on tensor.  Inference tensors have none (reading it raises):
+    they get a fresh token, so a cache entry on one never hits and the plan or check is redone
+    per call, which is always correct."""
+    return object() if t.is_inference() else t._version
+
+
 def _check_graph_once(row_ptr, col_idx, num_cols):
     """Out-of-range row_ptr / col_idx are the only inputs that can make a kernel read out of
     bounds, so each graph is validated the first time it is used; the check is cached on the
@@ -84,14 +91,14 @@ def _check_graph_once(row_ptr, col_idx, num_cols):
     hit = _CHECKED.get(key)
     if hit is not None:
         rr, cr, rv, cv, nc = hit
-        if rr() is row_ptr and cr() is col_idx and rv == row_ptr._version and \
-                cv == col_idx._version and nc == num_cols:
+        if rr() is row_ptr and cr() is col_idx and rv == _ver(row_ptr) and \
+                cv == _ver(col_idx) and nc == num_cols:
             return
     _validate_graph(row_ptr, col_idx, num_cols, col_idx.numel())
     if key not in _CHECKED:
         weakref.finalize(col_idx, _CHECKED.pop, key, None)
-    _CHECKED[key] = (weakref.ref(row_ptr), weakref.ref(col_idx), row_ptr._version,
-                     col_idx._version, int(num_cols))
+    _CHECKED[key] = (weakref.ref(row_ptr), weakref.ref(col_idx), _ver(row_ptr),
+                     _ver(col_idx), int(num_cols))
 
 
 def _validate_call(validate, row_ptr, col_idx, num_cols, sel, D):
@@ -269,7 +276,7 @@ def transpose_plan(indices: torch.Tensor, num_cols: int, cache: bool = True):
     hit = _PLAN_CACHE.get(key)
     if cache and hit is not None:
         ref, nc, ver, plan = hit
-        if ref() is indices and nc == num_cols and ver == indices._version:
+        if ref() is indices and nc == num_cols and ver == _ver(indices):
             return plan
     dev = indices.device
     E = indices.numel()
@@ -286,7 +293,7 @@ def transpose_plan(indices: torch.Tensor, num_cols: int, cache: bool = True):
     if cache:
         if key not in _PLAN_CACHE:
             weakref.finalize(indices, _PLAN_CACHE.pop, key, None)
-        _PLAN_CACHE[key] = (weakref.ref(indices), int(num_cols), indices._version, plan)
+        _PLAN_CACHE[key] = (weakref.ref(indices), int(num_cols), _ver(indices), plan)
     return plan
 
 
@@ -308,7 +315,7 @@ def bucket_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True
     hit = _BUCKET_CACHE.get(key)
     if cache and hit is not None:
         ref, nc, ver, plan = hit
-        if ref() is indices and nc == num_cols and ver == indices._version:
+        if ref() is indices and nc == num_cols and ver == _ver(indices):
             return plan
     dev = indices.device
     E = indices.numel()
@@ -326,7 +333,7 @@ def bucket_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True
     if cache:
         if key not in _BUCKET_CACHE:
             weakref.finalize(indices, _BUCKET_CACHE.pop, key, None)
-        _BUCKET_CACHE[key] = (weakref.ref(indices), int(num_cols), indices._version, plan)
+        _BUCKET_CACHE[key] = (weakref.ref(indices), int(num_cols), _ver(indices), plan)
     return plan
 
 
@@ -351,8 +358,8 @@ def bsort_plan(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int, k: in
     hit = _BSORT_CACHE.get(key)
     if cache and hit is not None:
         rp, ri, nc, pv, vi, plan = hit
-        if (rp() is indptr and ri() is indices and nc == num_cols and pv == indptr._version
-                and vi == indices._version):
+        if (rp() is indptr and ri() is indices and nc == num_cols and pv == _ver(indptr)
+                and vi == _ver(indices)):
             return plan
     dev = indices.device
     E = indices.numel()
@@ -376,7 +383,7 @@ def bsort_plan(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int, k: in
             for t in (indptr, indices):
                 weakref.finalize(t, _BSORT_CACHE.pop, key, None)
         _BSORT_CACHE[key] = (weakref.ref(indptr), weakref.ref(indices), int(num_cols),
-                             indptr._version, indices._version, plan)
+                             _ver(indptr), _ver(indices), plan)
     return plan
 
 
@@ -404,14 +411,15 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     if shift < 0:
         raise RuntimeError(f"pull_plan: invalid k {k}")
     num_rows = indptr.numel() - 1
-    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(dim), int(k)))
+    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(num_cols), int(dim),
+                                                              int(k)))
     key = (id(indptr), id(indices), id(values), shift, S)
     hit = _PULL_CACHE.get(key)
     if cache and hit is not None:
         rp, ri, rv, nc, pv, vi, vv, plan = hit
         if (rp() is indptr and ri() is indices and rv() is values and nc == num_cols
-                and pv == indptr._version and vi == indices._version
-                and vv == values._version):
+                and pv == _ver(indptr) and vi == _ver(indices)
+                and vv == _ver(values)):
             return plan
     dev = indices.device
     E = indices.numel()
@@ -430,7 +438,7 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
             for t in (indptr, indices, values):
                 weakref.finalize(t, _PULL_CACHE.pop, key, None)
         _PULL_CACHE[key] = (weakref.ref(indptr), weakref.ref(indices), weakref.ref(values),
-                            int(num_cols), indptr._version, indices._version, values._version,
+                            int(num_cols), _ver(indptr), _ver(indices), _ver(values),
                             plan)
     return plan
 
@@ -476,8 +484,8 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
     if cache and hit is not None:
         rp, ri, rv, nc, pv, vi, vv, plan = hit
         if (rp() is indptr and ri() is indices and rv() is values and nc == num_cols
-                and pv == indptr._version and vi == indices._version
-                and vv == values._version):
+                and pv == _ver(indptr) and vi == _ver(indices)
+                and vv == _ver(values)):
             return plan
     tptr, ent, shift, S = pull_plan(indptr, indices, values, num_cols, k, dim, cache=False)
     dev = indices.device
@@ -518,7 +526,7 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
             for t in (indptr, indices, values):
                 weakref.finalize(t, _HYBRID_CACHE.pop, key, None)
         _HYBRID_CACHE[key] = (weakref.ref(indptr), weakref.ref(indices), weakref.ref(values),
-                              int(num_cols), indptr._version, indices._version, values._version,
+                              int(num_cols), _ver(indptr), _ver(indices), _ver(values),
                               plan)
     return plan
 
@@ -548,7 +556,7 @@ def _scaled_entries(ent: torch.Tensor, tiles: Optional[torch.Tensor], tile_ent: 
     hit = _SCALED.get(key)
     if hit is not None:
         re, rd, ver, sc = hit
-        if re() is ent and rd() is row_div and ver == row_div._version:
+        if re() is ent and rd() is row_div and ver == _ver(row_div):
             return sc
     if ent.is_cuda and torch.cuda.is_current_stream_capturing():
         # a hipGraph capture records kernels without running them: a copy built here would
@@ -563,7 +571,7 @@ def _scaled_entries(ent: torch.Tensor, tiles: Optional[torch.Tensor], tile_ent: 
             _ptr(row_div), _ptr(sc), _stream(dev)), "maxk_pull_entries_scale")
     if key not in _SCALED:
         weakref.finalize(ent, _SCALED.pop, key, None)
-    _SCALED[key] = (weakref.ref(ent), weakref.ref(row_div), row_div._version, sc)
+    _SCALED[key] = (weakref.ref(ent), weakref.ref(row_div), _ver(row_div), sc)
     return sc
 
 
@@ -584,8 +592,8 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
     hit = _LOCALITY.get(key)
     if hit is not None:
         rp, ri, pv, iv, val = hit
-        if rp() is indptr and ri() is indices and pv == indptr._version and \
-                iv == indices._version:
+        if rp() is indptr and ri() is indices and pv == _ver(indptr) and \
+                iv == _ver(indices):
             return val
     _need(indptr, "indptr", torch.int32)
     _need(indices, "indices", torch.int32)
@@ -600,8 +608,8 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
     val = float(out.value)
     if key not in _LOCALITY:
         weakref.finalize(indices, _LOCALITY.pop, key, None)
-    _LOCALITY[key] = (weakref.ref(indptr), weakref.ref(indices), indptr._version,
-                      indices._version, val)
+    _LOCALITY[key] = (weakref.ref(indptr), weakref.ref(indices), _ver(indptr),
+                      _ver(indices), val)
     return val
 
 
@@ -962,31 +970,44 @@ def topk_cbsr(x: torch.Tensor, k: int, with_int32: bool = False):
         fn, name = L.maxk_topk_cbsr_u8, "maxk_topk_cbsr_u8"
     else:
         raise RuntimeError("Input must be float32 or uint8")
+    check = _checks_topk_rows(dev)
     with torch.cuda.device(dev):
         _capi.check(fn(_ptr(x), x.stride(0), _ptr(val), _ptr(idx), _ptr(idx32), V, D, k,
                        _stream(dev)), name)
-    _check_topk_rows(dev, name)
+    if check:
+        _check_topk_rows(dev, name)
     return (val, idx, idx32) if with_int32 else (val, idx)
 
 
 def topk_error_rows(device=None, reset: bool = True) -> int:
     """Rows whose top-k search took other than k winners on `device` since the last reset
-    (maxk_topk_error_rows; synchronises the device).  Always 0 unless the kernel has a bug: the
-    kernels count such a row and keep its writes inside its own k winner slots."""
+    (maxk_topk_error_rows; read in order on torch's current stream, which it synchronises).
+    Always 0 unless the kernel has a bug: the kernels count such a row and keep its writes
+    inside its own k winner slots."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
     n = ctypes.c_int64(0)
     with torch.cuda.device(dev):
-        _capi.check(_lib().maxk_topk_error_rows(ctypes.byref(n), 1 if reset else 0),
-                    "maxk_topk_error_rows")
+        _capi.check(_lib().maxk_topk_error_rows(ctypes.byref(n), 1 if reset else 0,
+                                                _stream(dev)), "maxk_topk_error_rows")
     return int(n.value)
 
 
+def _checks_topk_rows(dev) -> bool:
+    """MAXK_VALIDATE=1 outside a capture: zero the device's bad-row count before the launch
+    (a count left by an earlier unvalidated call is not this launch's), so the
+    read after it (_check_topk_rows) sees this launch's rows only.  Both run on the current
+    stream, in order with the launch."""
+    if not _validate_default() or torch.cuda.is_current_stream_capturing():
+        return False
+    topk_error_rows(dev, reset=True)
+    return True
+
+
 def _check_topk_rows(dev, name):
-    """MAXK_VALIDATE=1: raise if the launch just made left a row with other than k winners."""
-    if _validate_default() and not torch.cuda.is_current_stream_capturing():
-        bad = topk_error_rows(dev)
-        if bad:
-            raise RuntimeError(f"{name}: {bad} rows took other than k winners (kernel bug)")
+    """Raise if the launch just made left a row with other than k winners."""
+    bad = topk_error_rows(dev)
+    if bad:
+        raise RuntimeError(f"{name}: {bad} rows took other than k winners (kernel bug)")
 
 
 def cuda_topk_maxk(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -1039,11 +1060,13 @@ def topk_cbsr_dense(x: torch.Tensor, k: int):
     val = torch.empty(V, k, dtype=torch.float32, device=dev)
     idx = torch.empty(V, k, dtype=torch.uint8, device=dev)
     dense = torch.empty(V, D, dtype=torch.float32, device=dev)
+    check = _checks_topk_rows(dev)
     with torch.cuda.device(dev):
         _capi.check(_lib().maxk_topk_cbsr_dense(_ptr(x), x.stride(0), _ptr(val), _ptr(idx),
                                                 _ptr(dense), V, D, k, _stream(dev)),
                     "maxk_topk_cbsr_dense")
-    _check_topk_rows(dev, "maxk_topk_cbsr_dense")
+    if check:
+        _check_topk_rows(dev, "maxk_topk_cbsr_dense")
     return dense, val, idx
 
 

@@ -49,6 +49,7 @@ SIGNATURES = {
     "maxk_sspmm_backward_csc_sel": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64,
                                                _i64, _i32, _i32, _i32, _p, _sz, _p]),
     "maxk_edge_selectors": (ctypes.c_int, [_p, _p, _i64, _i32, _p, _p]),
+    "maxk_edge_selectors_blocks": (_i64, [_i64]),
     "maxk_transpose_plan_workspace_size": (_sz, [_i64, _i64]),
     "maxk_transpose_plan": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _sz, _p]),
     "maxk_sspmm_backward_bucket_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
@@ -75,7 +76,7 @@ SIGNATURES = {
                                                       _i32, _i32, _p, _i64, _i64, _i64, _i32,
                                                       _i32, _p, _sz, _p]),
     "maxk_pull_shift": (ctypes.c_int, [_i32]),
-    "maxk_pull_slices": (ctypes.c_int, [_i64, _i32, _i32]),
+    "maxk_pull_slices": (ctypes.c_int, [_i64, _i64, _i32, _i32]),
     "maxk_pull_plan_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32]),
     "maxk_pull_plan": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _sz,
                                       _p]),
@@ -95,7 +96,7 @@ SIGNATURES = {
                                                   _p]),
     "maxk_topk_cbsr": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_u8": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
-    "maxk_topk_error_rows": (ctypes.c_int, [_p, _i32]),
+    "maxk_topk_error_rows": (ctypes.c_int, [_p, _i32, _p]),
     "maxk_cbsr_scatter_dense": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_dense": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_backward": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i32, _i32, _p]),

@@ -24,9 +24,12 @@ torch.sparse / cuSPARSE fallback (a CPU fallback would void parity).
 
 Fixed caller-visible defects of the reference (DESIGN.md "Boundary"):
   * v1 backward unpacked 7 saved tensors out of 3 (ValueError); here it works;
-  * the backward divides by the same per-row divisor the forward used, so the
-    gradient is the exact adjoint (the reference divides by out_degrees; for
-    the symmetric graphs it targets in == out);
+  * the v1 backward divides by the same per-row divisor the forward used, so the
+    gradient is the exact adjoint; the reference divides G by out_degrees instead
+    (maxk_spgemm_function.py:154-159), which is the same on the symmetric graphs it
+    targets (in == out).  `backward_divisor="reference"` (keyword of maxk_spgemm /
+    MaxKSpmmWrapper.spmm, or the 12th apply() argument) reproduces the reference's
+    rule on any graph: G / out_degrees when given, else G undivided;
   * graph_indices_T / graph_values_T are accepted and unused: the kernel forms
     the A^T product from the CSR itself.
 """
@@ -62,7 +65,12 @@ def _converted(src, tag, make):
     """make(src), cached per source tensor object and version: the backward's plans and the
     auto mode's locality pass are cached on the identity of the int32 / fp32 tensors they see,
     so an int64 indptr, a warp4 array or float64 values converted afresh every step would
-    rebuild them (and re-synchronise the host) on every call."""
+    rebuild them (and re-synchronise the host) on every call.  Graph-side tensors
+    only (indices, indptr, edge values, warp4, degrees): activations are converted uncached
+    (_f32_act), so no fp32 copy of a [V, D] input outlives its call.  Inference
+    tensors carry no version counter and are converted uncached too."""
+    if src.is_inference() or torch.is_inference_mode_enabled():
+        return make(src)
     key = (id(src), tag)
     hit = _CONVERTED.get(key)
     if hit is not None:
@@ -94,11 +102,19 @@ def _indptr_for(graph_indptr, warp4_metadata, num_warps, num_v):
 
 
 def _f32(t):
+    """Graph-side fp32 tensor (edge values, degrees), conversion cached per source tensor."""
     if t is None:
         return None
     if t.dtype == torch.float32 and t.is_contiguous():
         return t
     return _converted(t, "f32", lambda u: u.float().contiguous())
+
+
+def _f32_act(t):
+    """Activation (input features, top-k values): converted afresh, never cached."""
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t
+    return t.float().contiguous()
 
 
 def _edge_sel_for(indptr, indices, k, num_cols, D):
@@ -129,8 +145,9 @@ class MaxKSpGEMMFunction(Function):
     @staticmethod
     def _forward_v1(ctx, graph_indices, graph_values, input_features, k_value,
                     warp4_metadata=None, num_warps=0, graph_indptr=None, in_degrees=None,
-                    out_degrees=None, graph_indices_T=None, graph_values_T=None):
-        x = _f32(input_features)
+                    out_degrees=None, graph_indices_T=None, graph_values_T=None,
+                    backward_divisor=None):
+        x = _f32_act(input_features)
         V, D = x.shape
         k = int(k_value)
         if k < D:
@@ -142,15 +159,21 @@ class MaxKSpGEMMFunction(Function):
                 .unsqueeze(0).expand(V, -1).contiguous()
         indptr = _indptr_for(graph_indptr, warp4_metadata, num_warps, V)
         row_div = _f32(in_degrees)
+        if backward_divisor not in (None, "adjoint", "reference"):
+            raise ValueError(f"backward_divisor must be 'adjoint' or 'reference', "
+                             f"got {backward_divisor!r}")
+        # the backward's divisor of G's rows: the forward's own (the exact adjoint), or the
+        # reference's rule, G / out_degrees when given and G undivided otherwise (:154-159)
+        bwd_div = _f32(out_degrees) if backward_divisor == "reference" else row_div
         es, ctx.es_mode = _edge_sel_for(indptr, graph_indices, k, V, D)
         out = maxk_cuda_kernels.spgemm_forward(indptr, graph_indices, _f32(graph_values),
                                                sparse_data, sparse_selector, D, row_div=row_div,
                                                edge_sel_out=es)
         ctx.shape_v1 = (V, D)
         ctx.save_for_backward(indptr, graph_indices, graph_values, sparse_selector,
-                              row_div if row_div is not None else torch.empty(0),
+                              bwd_div if bwd_div is not None else torch.empty(0),
                               es if es is not None else torch.empty(0))
-        ctx.has_div = row_div is not None
+        ctx.has_div = bwd_div is not None
         ctx.has_es = es is not None
         ctx.mode = "v1"
         return out
@@ -160,7 +183,7 @@ class MaxKSpGEMMFunction(Function):
     def _forward_v4(ctx, graph_indices, graph_values, topk_values, topk_indices,
                     warp4_metadata=None, num_warps=0, graph_indptr=None, degrees=None,
                     dim_origin=None):
-        vals = _f32(topk_values)
+        vals = _f32_act(topk_values)
         sel = topk_indices if topk_indices.dtype == torch.uint8 else topk_indices.to(torch.uint8)
         sel = sel.contiguous()
         V, k = vals.shape
@@ -204,7 +227,9 @@ def maxk_spgemm(graph_indices, graph_values, a3, a4, *rest, **kw):
     """Both shapes (see module doc):
     v1: maxk_spgemm(graph_indices, graph_values, input_features, k_value, warp4_metadata=None,
                     num_warps=0, graph_indptr=None, in_degrees=None, out_degrees=None,
-                    graph_indices_T=None, graph_values_T=None)
+                    graph_indices_T=None, graph_values_T=None, backward_divisor=None)
+        backward_divisor: None / "adjoint" (G / in_degrees, the exact gradient) or
+        "reference" (G / out_degrees, the reference's rule, maxk_spgemm_function.py:154-159)
     v4: maxk_spgemm(graph_indices, graph_values, topk_values, topk_indices, warp4_metadata,
                     num_warps, graph_indptr, degrees, dim_origin=None)"""
     _require_kernels()
@@ -213,8 +238,8 @@ def maxk_spgemm(graph_indices, graph_values, a3, a4, *rest, **kw):
         defaults = (None, 0, None, None, None)
     else:
         names = ("warp4_metadata", "num_warps", "graph_indptr", "in_degrees", "out_degrees",
-                 "graph_indices_T", "graph_values_T")
-        defaults = (None, 0, None, None, None, None, None)
+                 "graph_indices_T", "graph_values_T", "backward_divisor")
+        defaults = (None, 0, None, None, None, None, None, None)
     args = list(rest) + [None] * (len(names) - len(rest))
     for i, n in enumerate(names):
         if n in kw:
@@ -223,7 +248,7 @@ def maxk_spgemm(graph_indices, graph_values, a3, a4, *rest, **kw):
             args[i] = defaults[i]
     if kw:
         raise TypeError(f"unexpected keyword arguments: {sorted(kw)}")
-    if isinstance(a4, torch.Tensor) and args[-1] is None:
+    if args[-1] is None:  # dim_origin / backward_divisor left out: the reference's arity
         args = args[:-1]
     return MaxKSpGEMMFunction.apply(graph_indices, graph_values, a3, a4, *args)
 
@@ -281,7 +306,7 @@ class MaxKSpmmWrapper:
             names = ("graph_indptr", "degrees", "dim_origin")
         else:
             names = ("graph_indptr", "in_degrees", "out_degrees", "graph_indices_T",
-                     "graph_values_T")
+                     "graph_values_T", "backward_divisor")
         vals = dict(zip(names, rest))
         vals.update(kw)
         ip = self._indptr(vals.get("graph_indptr"), a3.shape[0])
@@ -291,4 +316,5 @@ class MaxKSpmmWrapper:
                                dim_origin=vals.get("dim_origin"))
         return maxk_spgemm(graph_indices, graph_values, a3, a4, self.warp4_metadata,
                            self.num_warps, ip, vals.get("in_degrees"), vals.get("out_degrees"),
-                           vals.get("graph_indices_T"), vals.get("graph_values_T"))
+                           vals.get("graph_indices_T"), vals.get("graph_values_T"),
+                           backward_divisor=vals.get("backward_divisor"))

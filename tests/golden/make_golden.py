@@ -17,6 +17,13 @@ What runs from the reference (imported read-only from /root/reference, CPU only)
 The prebuilt maxk_cuda_kernels*.so that ships in the reference is never loaded:
 sys.modules is primed so that `import maxk_cuda_kernels` raises ImportError.
 
+asym_outdeg_d256_k16 additionally pins the v1 backward's divisor on a graph whose in- and
+out-degrees differ: `grad_cbsr_refrule` is the gradient the reference's
+hand-written backward intends -- grad_output / out_degrees through the A^T product, no
+in-degree division (maxk_spgemm_function.py:154-175) -- obtained by autograd through the
+reference forward called without in_degrees and fed G / out_degrees; `grad_cbsr_ref` stays the
+exact adjoint of the normalised forward.
+
 Fixtures hold data only: inputs (CSR, edge weights, features, degrees, upstream
 grad) and the reference's outputs.  Inputs are continuous random values, so
 torch.topk has no ties and index vectors are well defined.
@@ -91,10 +98,12 @@ CASES = [
     ("flickr_d64_k16", 1500, 11, True,  True,  ((0, 500),),               0,     64,  16),
     ("odd_d100_k10",  257,  9,   False, False, ((1, 200),),               7,     100, 10),
     ("tiny_d64_k4",   40,   3,   True,  False, (),                        5,     64,  4),
+    ("asym_outdeg_d256_k16", 500, 16, False, True, ((2, 450), (33, 120)),   12,    256, 16),
 ]
+OUTDEG = {"asym_outdeg_d256_k16"}
 
 
-def gen_case(ref_fn, ref_meta, name, V, avg, sym, loops, hubs, empty, D, k, seed):
+def gen_case(ref_fn, ref_meta, name, V, avg, sym, loops, hubs, empty, D, k, seed):  # noqa: C901
     rng = np.random.default_rng(seed)
     row_ptr, col_idx = make_graph(rng, V, avg, sym, loops, hubs, empty)
     E = col_idx.size
@@ -123,7 +132,7 @@ def gen_case(ref_fn, ref_meta, name, V, avg, sym, loops, hubs, empty, D, k, seed
     off = grad_x.copy()
     np.put_along_axis(off, sel.astype(np.int64), 0.0, axis=1)
     assert not off.any()
-    return dict(
+    out = dict(
         row_ptr=row_ptr, col_idx=col_idx, val=val, x=x, g=g, deg=deg,
         k=np.int32(k), D=np.int32(D),
         y_ref=y.detach().numpy(),
@@ -131,13 +140,27 @@ def gen_case(ref_fn, ref_meta, name, V, avg, sym, loops, hubs, empty, D, k, seed
         grad_cbsr_ref=grad_cbsr,
         warp4_ref=np.asarray(w4, dtype=np.int32),
     )
+    if name in OUTDEG:
+        out_deg = np.maximum(np.bincount(col_idx, minlength=V), 1).astype(np.float32)
+        assert not np.array_equal(out_deg, deg)
+        t_x2 = torch.from_numpy(x.copy()).requires_grad_(True)
+        with contextlib.redirect_stdout(io.StringIO()):
+            y2 = ref_fn.MaxKSpGEMMFunction.forward(
+                _Ctx(), t_idx, t_val, t_x2, k, None, 0, t_indptr, None, None, None, None)
+        y2.backward(torch.from_numpy(g.copy()) / torch.from_numpy(out_deg).unsqueeze(-1))
+        out["out_deg"] = out_deg
+        out["grad_cbsr_refrule"] = np.take_along_axis(t_x2.grad.numpy(), sel.astype(np.int64),
+                                                      axis=1)
+    return out
 
 
-def main():
+def main(only=None):
     torch.manual_seed(0)
     ref_fn, ref_meta = _import_reference()
     for i, case in enumerate(CASES):
         name = case[0]
+        if only and name not in only:
+            continue
         data = gen_case(ref_fn, ref_meta, *case, seed=1000 + i)
         path = os.path.join(OUT, f"{name}.npz")
         np.savez_compressed(path, **data)
@@ -146,4 +169,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(set(sys.argv[1:]))  # optional case names: regenerate only those

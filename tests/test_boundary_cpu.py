@@ -235,18 +235,23 @@ def test_pull_slice_rule():
     buckets, k] per slice."""
     from maxk_cuda_kernels import _capi
     L = _capi.load()
-    assert L.maxk_pull_slices(232965, 256, 16) == 28  # Reddit: 238.6 MB of G rows, 2 parts
-    assert L.maxk_pull_slices(232965, 256, 8) == 44   # 1 part
-    assert L.maxk_pull_slices(232965, 256, 32) == 33  # 2 parts
-    assert L.maxk_pull_slices(232965, 256, 64) == 22  # 4 parts, factor capped at 3
-    assert L.maxk_pull_slices(29121, 256, 16) == 4    # one of 8 row shards
-    assert L.maxk_pull_slices(1, 256, 16) == 1 and L.maxk_pull_slices(0, 256, 16) == 1
-    assert L.maxk_pull_slices(100_000_000, 256, 16) == 256
-    assert L.maxk_pull_slices(2_449_029, 256, 64) == 228
-    assert L.maxk_pull_slices(4_000_000, 16, 64) == 62  # rows in a slice stay <= 65536
+    assert L.maxk_pull_slices(232965, 0, 256, 16) == 28  # Reddit: 238.6 MB of G rows, 2 parts
+    assert L.maxk_pull_slices(232965, 0, 256, 8) == 44   # 1 part
+    assert L.maxk_pull_slices(232965, 0, 256, 32) == 33  # 2 parts
+    assert L.maxk_pull_slices(232965, 0, 256, 64) == 22  # 4 parts, factor capped at 3
+    assert L.maxk_pull_slices(29121, 0, 256, 16) == 4    # one of 8 row shards
+    assert L.maxk_pull_slices(1, 0, 256, 16) == 1 and L.maxk_pull_slices(0, 0, 256, 16) == 1
+    assert L.maxk_pull_slices(100_000_000, 0, 256, 16) == 256
+    assert L.maxk_pull_slices(2_449_029, 0, 256, 64) == 228
+    assert L.maxk_pull_slices(4_000_000, 0, 16, 64) == 62  # rows in a slice stay <= 65536
     # Flickr-sized (89k rows, D = 64): 132 / 352 / 264 tiles at k = 16 / 32 / 64 would leave
     # a nearly empty last round of workgroups; the slices drop to 2 (k = 8 keeps 5: 220, one round)
-    assert [L.maxk_pull_slices(89250, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
+    assert [L.maxk_pull_slices(89250, 0, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
+    assert [L.maxk_pull_slices(89250, 89250, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
+    # a rectangular shard (a quarter of the rows, every column): rounds counted over the
+    # columns' buckets, not the rows'
+    assert L.maxk_pull_slices(44625, 0, 256, 8) == 9
+    assert L.maxk_pull_slices(44625, 89250, 256, 8) == 5
     gp = (232965 * 256 * 4 + 255) // 256 * 256
     selq = 2 * ((232965 * 16 + 255) // 256 * 256)  # slot-ordered selectors + their l map
     assert L.maxk_sspmm_backward_pull_workspace_size(232965, 232965, 256, 16, 65) == \
@@ -265,3 +270,47 @@ def test_edge_selector_rule(monkeypatch):
     assert mk.edge_selectors_wanted(64) and not mk.edge_selectors_wanted(10)
     monkeypatch.setenv("MAXK_EDGE_SEL", "0")
     assert not mk.edge_selectors_wanted(8)
+
+
+def test_edge_selector_grid_capped():
+    """maxk_edge_selectors walks its words grid-stride over a capped grid, so
+    num_e * k one-byte words past 2^32 (products-sized graphs at k = 64 with unaligned
+    streams) still fit one grid dimension."""
+    from maxk_cuda_kernels import _capi
+    lib = _capi.load()
+    assert lib.maxk_edge_selectors_blocks(0) == 0
+    assert lib.maxk_edge_selectors_blocks(1) == 1
+    assert lib.maxk_edge_selectors_blocks(256 * 1000) == 1000
+    for n_words in (1 << 32, 123_718_280 * 64, 1 << 40):
+        b = lib.maxk_edge_selectors_blocks(n_words)
+        assert 0 < b and b * 256 < (1 << 32) and b <= 256 * 64
+
+
+def test_bench_launches_its_own_ranks(monkeypatch):
+    """`python bench.py --gpus N` with no WORLD_SIZE (the driver's BENCH command shape at
+    N > 1) starts the N ranks as a child torch.distributed.run on 127.0.0.1 and exits with its
+    status; nothing here touches a GPU (the child command is captured, not run)."""
+    import subprocess
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("MAXK_DIST_BACKEND", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "3", "--warmup", "1"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-6:] == ["--gpus", "8", "--steps", "3", "--warmup", "1"]
+    assert cmd[-7].endswith("bench.py")
+    # no GPU here: fewer visible devices than ranks -> gloo-staged collectives
+    assert seen["env"]["MAXK_DIST_BACKEND"] == "gloo"

@@ -151,6 +151,20 @@ def test_train_bench_matches_library(cuda):
 
 
 @pytest.mark.gpu
+def test_train_bench_products_epoch(cuda):
+    """BASELINE.json configs[2] at its real shape: the 3-layer MaxK-SAGE
+    (hidden 256, k = 32) on the ogbn-products-sized graph (V = 2,449,029, E = 123.7M), two
+    epochs on the HIP aggregation and two on rocSPARSE from the same weights: the first loss
+    (forward) within 1e-4 and the second (after an Adam step on each side's gradients) within
+    1e-3."""
+    import maxk_train_bench
+    out = maxk_train_bench.main(["products", "--k", "32", "--epochs", "2", "--warmup", "0"])
+    assert out["V"] == 2449029 and out["hidden"] == 256 and out["layers"] == 3
+    assert out["loss_match"], out
+    assert out["last_loss_match"], out
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("model_cls", ["MaxKGCN", "MaxKGIN"])
 def test_gcn_gin_models(cuda, model_cls):
     """The GCN / GIN models (model_integrated_v3.py:590-752) on the HIP aggregation vs the

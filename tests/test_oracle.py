@@ -61,6 +61,19 @@ def test_warp4_matches_reference(path):
     assert np.array_equal(O.warp4(z["row_ptr"], 64), z["warp4_ref"])
 
 
+def test_backward_reference_divisor_rule():
+    """asym_outdeg_d256_k16: in- and out-degrees differ; the reference's v1 backward rule
+    (grad_output / out_degrees through A^T, maxk_spgemm_function.py:154-175) is the oracle's
+    backward with row_div = out_degrees, and differs from the exact adjoint there."""
+    import os
+    from conftest import GOLDEN
+    z = load_golden(os.path.join(GOLDEN, "asym_outdeg_d256_k16.npz"))
+    gs = O.sspmm_bwd(z["row_ptr"], z["col_idx"], z["val"], z["g"], z["topk_idx"],
+                     row_div=z["out_deg"])
+    assert close(gs, z["grad_cbsr_refrule"])
+    assert not close(gs, z["grad_cbsr_ref"])
+
+
 def test_oracle_adjoint_identity():
     """<A.scatter(v), G> == <v, gather(A^T G)>: forward and backward are adjoint."""
     z = load_golden(CASES[0])

@@ -468,6 +468,56 @@ def test_autograd_v1_golden(F, cuda, path):
     close(x.grad, ref)
 
 
+@pytest.mark.parametrize("via", ["function", "wrapper"])
+def test_autograd_v1_out_degrees(F, cuda, via):
+    """a graph whose in- and out-degrees differ.  By default the v1
+    backward is the exact adjoint of the normalised forward (G / in_degrees); with
+    backward_divisor="reference" it follows the reference's rule, G / out_degrees
+    (maxk_spgemm_function.py:154-159), both against fixtures made by the reference's code."""
+    from conftest import GOLDEN
+    z = load_golden(f"{GOLDEN}/asym_outdeg_d256_k16.npz")
+    D = int(z["D"])
+    ip, col, val = T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda)
+    din, dout = T(z["deg"], cuda), T(z["out_deg"], cuda)
+    w = F.MaxKSpmmWrapper("outdeg")
+    assert w.build_metadata(ip)
+    for rule, want in ((None, "grad_cbsr_ref"), ("adjoint", "grad_cbsr_ref"),
+                       ("reference", "grad_cbsr_refrule")):
+        x = T(z["x"], cuda).requires_grad_(True)
+        kw = {} if rule is None else {"backward_divisor": rule}
+        if via == "function":
+            y = F.maxk_spgemm(col, val, x, int(z["k"]), graph_indptr=ip, in_degrees=din,
+                              out_degrees=dout, **kw)
+        else:
+            y = w.spmm(col, val, x, int(z["k"]), ip, din, dout, **kw)
+        close(y, z["y_ref"])
+        y.backward(T(z["g"], cuda))
+        close(x.grad, O.scatter_dense(z[want], z["topk_idx"], D))
+    with pytest.raises(ValueError):
+        F.maxk_spgemm(col, val, T(z["x"], cuda), int(z["k"]), graph_indptr=ip,
+                      backward_divisor="out")
+
+
+def test_autograd_v1_inference_mode_bf16(F, cuda):
+    """a bf16 (or non-contiguous) activation under torch.inference_mode() goes
+    through the v1 path (its fp32 copy is made per call, never cached), and equals the fp32
+    call on the same values."""
+    from conftest import GOLDEN
+    import maxk_spgemm_function as Fm
+    z = load_golden(f"{GOLDEN}/sym_d256_k16.npz")
+    ip, col, val = T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda)
+    deg = T(z["deg"], cuda)
+    xb = T(z["x"], cuda).to(torch.bfloat16)
+    n0 = len(Fm._CONVERTED)
+    with torch.inference_mode():
+        y = F.maxk_spgemm(col, val, xb, int(z["k"]), graph_indptr=ip, in_degrees=deg)
+        y_nc = F.maxk_spgemm(col, val, xb.float().t().contiguous().t(), int(z["k"]),
+                             graph_indptr=ip.long(), in_degrees=deg.double())
+    assert len(Fm._CONVERTED) == n0  # nothing cached: inference tensors, activations
+    y32 = F.maxk_spgemm(col, val, xb.float(), int(z["k"]), graph_indptr=ip, in_degrees=deg)
+    assert torch.equal(y, y32.detach()) and torch.equal(y_nc, y32.detach())
+
+
 @pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_autograd_v4_wrapper_golden(F, cuda, path):
     z = load_golden(path)

@@ -45,7 +45,7 @@ SHORT="bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-rocsparse --no-cpu-
 
 step_tests() {
   mkdir -p $O
-  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --durations=25 \
     --timeout-method thread > $O/pytest_gpu.log 2>&1
   tail -2 $O/pytest_gpu.log
 }
