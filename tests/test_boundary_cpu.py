@@ -314,3 +314,27 @@ def test_bench_launches_its_own_ranks(monkeypatch):
     assert cmd[-7].endswith("bench.py")
     # no GPU here: fewer visible devices than ranks -> gloo-staged collectives
     assert seen["env"]["MAXK_DIST_BACKEND"] == "gloo"
+
+
+def test_bench_binding_roofline_and_traffic_order():
+    """roofline.binding: the launch's floor is the largest of the HBM,
+    Infinity-Cache-line and tag-rate terms, its fraction at most 1 for a launch no faster
+    than the floor; counters are read from the newest round, its final build first."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    files = [os.path.relpath(p, ROOT) for p in bench.traffic_files()]
+    rounds = [int(p.split(os.sep)[1][1:]) for p in files]
+    assert rounds == sorted(rounds, reverse=True)
+    for i, p in enumerate(files[:-1]):
+        nxt = files[i + 1]
+        if p.split(os.sep)[1] == nxt.split(os.sep)[1]:  # same round: final/ first
+            assert p.endswith(os.path.join("final", "traffic.json"))
+    rec = {"bytes": 13.0e9, "tag_accesses": 1.13e9}
+    b = bench.binding_roofline(2.1248, 1.175e9, rec)
+    assert b["bound"] == "tag_rate" and 0 < b["frac"] <= 1
+    assert b["terms_ms"]["fabric_lines"] == round(13.0e9 / 8.6e12 * 1e3, 4)
+    b = bench.binding_roofline(1.59, 1.2e9, {"bytes": 11.9e9})
+    assert b["bound"] == "fabric_lines" and b["frac"] <= 1
+    b = bench.binding_roofline(1.0, 1e9, None)
+    assert b["bound"] == "hbm_compulsory" and b["frac"] == 0.125

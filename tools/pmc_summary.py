@@ -9,6 +9,9 @@ bytes (MI355X_MICROARCH.md, HBM) -- the corrected column doubles it.
 With --traffic-out, per-op HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE summed over
 the op's kernels, bench.OP_KERNELS) are merged into that JSON under WORKLOAD (bench.py's
 traffic_key, e.g. reddit-D256-k16-csc-n1), where bench.py reads them as roofline.traffic.
+When the CSVs also hold a TCP_TOTAL_CACHE_ACCESSES_sum pass (the texture path's tag
+accesses, r05), the op's tag accesses per launch go beside them ("tag_accesses"), and
+GRBM_GUI_ACTIVE ("gui_active", summed over the 8 XCDs): bench.py's roofline.binding.
 """
 import argparse
 import collections
@@ -53,6 +56,11 @@ def main():
             extra = f"  -> {m * 1024 / 1e9:.3f} GB raw, {2 * m * 1024 / 1e9:.3f} GB x2-corrected"
         elif c == "WRITE_SIZE":
             extra = f"  -> {m * 1024 / 1e9:.3f} GB"
+        if c in ("TCP_TOTAL_CACHE_ACCESSES_sum", "GRBM_GUI_ACTIVE"):
+            prev = per_kernel[base(k)].get(c)
+            if prev is None or len(v) > n_disp[(base(k), c)]:
+                per_kernel[base(k)][c] = m
+                n_disp[(base(k), c)] = len(v)
         if c in ("FETCH_SIZE", "WRITE_SIZE"):
             # template variants of one kernel (e.g. a validating call's plain forward beside
             # the timed emitting one): the variant with the most dispatches stands for it
@@ -76,6 +84,11 @@ def main():
             w = sum(per_kernel.get(k, {}).get("WRITE_SIZE", 0.0) for k in ks)
             ops[op] = {"bytes": int(2 * f + w), "fetch_raw": int(f), "write": int(w),
                        "kernels": {k: per_kernel.get(k, {}) for k in ks}}
+            tags = [per_kernel.get(k, {}).get("TCP_TOTAL_CACHE_ACCESSES_sum") for k in ks]
+            if any(t is not None for t in tags):
+                ops[op]["tag_accesses"] = int(sum(t or 0.0 for t in tags))
+                ops[op]["gui_active"] = int(sum(per_kernel.get(k, {}).get("GRBM_GUI_ACTIVE", 0.0)
+                                                for k in ks))
         out[a.key] = ops
         with open(a.traffic_out, "w") as fh:
             json.dump(out, fh, indent=1, sort_keys=True)

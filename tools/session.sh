@@ -64,11 +64,15 @@ step_stats() {
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-format csv \
     -- python3 $SHORT > $O/stats_bench.json 2> $O/stats_bench.err
 }
+# PMC passes: FETCH_SIZE, WRITE_SIZE, and the texture path's tag accesses with the XCD clocks
+# (roofline.binding, r05); one rocprofv3 --pmc run each, named by the first counter
+PASSES="FETCH_SIZE WRITE_SIZE TCP_TOTAL_CACHE_ACCESSES_sum:GRBM_GUI_ACTIVE"
 step_pmc() {
   mkdir -p $O
-  for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --pmc $c -d $O/pmc_$c -o run --output-format csv \
-      -- python3 $SHORT > $O/pmc_$c.json 2> $O/pmc_$c.err
+  local c
+  for c in $PASSES; do
+    timeout -k 10 300 rocprofv3 --pmc ${c//:/ } -d $O/pmc_${c%%:*} -o run --output-format csv \
+      -- python3 $SHORT > $O/pmc_${c%%:*}.json 2> $O/pmc_${c%%:*}.err
   done
 }
 preset() {  # preset <name> <bench args...>
@@ -117,10 +121,11 @@ stats_one() {
 }
 pmc_one() {
   local c
-  for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --pmc $c -d $O/pmc_cfg/${1}_$c -o run --output-format csv \
-      -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-cpu-spmm --no-rocsparse \
-      $2 > $O/pmc_cfg/${1}_$c.json 2> $O/pmc_cfg/${1}_$c.err
+  for c in $PASSES; do
+    timeout -k 10 300 rocprofv3 --pmc ${c//:/ } -d $O/pmc_cfg/${1}_${c%%:*} -o run \
+      --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline \
+      --no-cpu-spmm --no-rocsparse $2 > $O/pmc_cfg/${1}_${c%%:*}.json \
+      2> $O/pmc_cfg/${1}_${c%%:*}.err
   done
   echo "$1 done"
 }
@@ -251,7 +256,12 @@ step_collect() {
   if [ -f $O/pmc_FETCH_SIZE/run_counter_collection.csv ]; then
     cp $O/pmc_FETCH_SIZE/run_counter_collection.csv $P/pmc_fetch_size.csv
     cp $O/pmc_WRITE_SIZE/run_counter_collection.csv $P/pmc_write_size.csv
-    python tools/pmc_summary.py $P/pmc_fetch_size.csv $P/pmc_write_size.csv \
+    local tags=""
+    if [ -f $O/pmc_TCP_TOTAL_CACHE_ACCESSES_sum/run_counter_collection.csv ]; then
+      cp $O/pmc_TCP_TOTAL_CACHE_ACCESSES_sum/run_counter_collection.csv $P/pmc_tags.csv
+      tags=$P/pmc_tags.csv
+    fi
+    python tools/pmc_summary.py $P/pmc_fetch_size.csv $P/pmc_write_size.csv $tags \
       --traffic-out $P/traffic.json \
       --key "$(python -c "import json; print(json.load(open('$O/pmc_FETCH_SIZE.json'))['roofline']['traffic_key'])")" \
       > $P/pmc_summary.txt
@@ -260,7 +270,9 @@ step_collect() {
     for j in $O/pmc_cfg/*_FETCH_SIZE.json; do
       local n=$(basename $j _FETCH_SIZE.json)
       python tools/pmc_summary.py $O/pmc_cfg/${n}_FETCH_SIZE/run_counter_collection.csv \
-        $O/pmc_cfg/${n}_WRITE_SIZE/run_counter_collection.csv --traffic-out $P/traffic.json \
+        $O/pmc_cfg/${n}_WRITE_SIZE/run_counter_collection.csv \
+        $(ls $O/pmc_cfg/${n}_TCP_TOTAL_CACHE_ACCESSES_sum/run_counter_collection.csv 2>/dev/null) \
+        --traffic-out $P/traffic.json \
         --key "$(python -c "import json; print(json.load(open('$j'))['roofline']['traffic_key'])")" \
         > $P/pmc_summary_$n.txt
     done
