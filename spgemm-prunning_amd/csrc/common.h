@@ -32,6 +32,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_FWD_SHORT  // forward: rows of at most this many edges go in batches of 64/KG
 #define MAXK_FWD_SHORT 16  // (one row per lane group); 0 = off
 #endif
+#ifndef MAXK_FWD_STREAM  // forward, sparse graphs: lane groups stream rows of at most this many
+#define MAXK_FWD_STREAM 64  // edges each (stream_rows); 0 = off (the short-row batches)
+#endif
 #ifndef MAXK_FWD_WAVES
 #define MAXK_FWD_WAVES 1
 #endif
@@ -103,6 +106,15 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #endif
 #ifndef MAXK_TOPK_LB  // four-row top-k: bit search from a lower bound of the k-th key
 #define MAXK_TOPK_LB 1
+#endif
+#ifndef MAXK_PULL_DIRECT  // small graphs: the pull in one launch (maxk_pull_direct)
+#define MAXK_PULL_DIRECT 1
+#endif
+#ifndef MAXK_PULL_DIRECT_EDGES  // ... up to this many edges
+#define MAXK_PULL_DIRECT_EDGES (8 << 20)
+#endif
+#ifndef MAXK_PULL_DIRECT_WGS  // ... with buckets sized for this many workgroups per CU
+#define MAXK_PULL_DIRECT_WGS 2
 #endif
 #ifndef MAXK_PULL_SEL4  // pull_sel4_kernel: four selectors per thread (aligned selectors)
 #define MAXK_PULL_SEL4 1

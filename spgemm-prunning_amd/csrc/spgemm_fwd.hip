@@ -442,7 +442,141 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
     wave_lds_fence();
 }
 
-template <int KG, int U, bool WIDE, bool EMIT>
+// Streaming rows (r05; sparse graphs: KG >= 16, so a lane group covers a D = 64 row with one
+// 16-B access per lane).  Each lane group walks whole rows on its own, U edges per step, and
+// takes the item's next row the step its current one ends, so the wave keeps NC rows in flight
+// with no batch boundary; the next step's columns and weights (and a new row's divisor) are
+// loaded while this step's records are in flight.  A row then costs about one dependent round
+// of loads per U edges, against two in the batched path (columns, then records), which on a
+// small sparse graph -- one round of waves, each a chain of such rounds -- is the whole time.
+// A group flushes its finished row from its own LDS copy (16-B stores).  Rows are taken in
+// order while the next one is owned by the item (token < d1) and has at most lmax edges;
+// returns the first row not taken (the caller walks a longer one with the whole wave).  Copies
+// are zero on entry and on return.
+template <int KG, int U>
+__device__ __forceinline__ int stream_rows(float *acc, int DS, int r,
+                                           const int32_t *__restrict__ row_ptr, int num_rows,
+                                           int64_t d1, const int32_t *__restrict__ col_idx,
+                                           const float *__restrict__ edge_val,
+                                           const uint8_t *__restrict__ rec, int RS,
+                                           const float *__restrict__ row_div,
+                                           float *__restrict__ out, int D, int k, int trash,
+                                           int lane, int flags, int lmax, int64_t num_e) {
+    constexpr int NC = kWave / KG;
+    const int g = lane / KG, l0 = lane % KG;
+    float *acc_g = acc + g * DS;
+    const bool lok = l0 < k;
+    const uint32_t vo = 4u * (uint32_t)(lok ? l0 : k - 1);
+    const uint32_t so = 4u * (uint32_t)k + 2u * (uint32_t)(lok ? l0 : k - 1);
+    const bool add = flags & 1, nt = flags & 2;
+    // row_ptr window: rows [wb, wb + 64), one per lane
+    int wb = r;
+    int rpw = row_ptr[wb + lane <= num_rows ? wb + lane : num_rows];
+    const int ebase = __builtin_amdgcn_readfirstlane(rpw);  // = row_ptr[r]
+    const int64_t span = (num_e - ebase) * 4;
+    const auto crs = wave_buffer(col_idx + ebase, (uint32_t)(span < 0xffffffffLL ? span : 0xffffffffLL));
+    const auto vrs = wave_buffer(edge_val + ebase, (uint32_t)(span < 0xffffffffLL ? span : 0xffffffffLL));
+    const auto rrs = wave_buffer(rec, 0xffffffffu);  // offsets < num_cols * RS < 2^32
+    int next = r;       // the next row to hand out (wave-uniform)
+    bool stop = false;  // the next row is not the item's or is too long (wave-uniform)
+    int row = -1, e = 0, ee = 0;  // this group's row and its edge range [e, ee)
+    float div = 1.f;
+    auto assign = [&]() {
+        const uint64_t idle = __ballot(row < 0);
+#pragma unroll
+        for (int gi = 0; gi < NC; ++gi) {
+            if (stop || !((idle >> (gi * KG)) & 1ull)) continue;
+            if (next + 1 >= wb + kWave) {  // slide the window (wave-uniform)
+                wb = next;
+                rpw = row_ptr[wb + lane <= num_rows ? wb + lane : num_rows];
+            }
+            const int a = __builtin_amdgcn_readlane(rpw, next - wb);
+            const int b = __builtin_amdgcn_readlane(rpw, next + 1 - wb);
+            if (next < num_rows && (int64_t)next + a < d1 && b - a <= lmax) {
+                if (g == gi) {
+                    row = next;
+                    e = a;
+                    ee = b;
+                    div = row_div ? row_div[next] : 1.f;  // arrives long before the flush
+                }
+                ++next;
+            } else {
+                stop = true;
+            }
+        }
+    };
+    auto load_cw = [&](int (&c)[U], float (&w)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int off = row >= 0 && e + u < ee ? (e + u - ebase) * 4 : (int)0x80000000;
+            c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, off, 0, 0);
+            w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, off, 0, 0));
+        }
+    };
+    assign();
+    int c[U];
+    float w[U];
+    load_cw(c, w);
+    int cn[U];  // placeholder for load_cw's signature: the next columns go straight into c
+    float wn[U];
+    while (__ballot(row >= 0)) {
+        float v[U];
+        int s[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t ro = __umul24((uint32_t)c[u], (uint32_t)RS);
+            v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, (int)(ro + vo), 0, 0));
+            s[u] = __builtin_amdgcn_raw_buffer_load_b16(rrs, (int)(ro + so), 0, 0);
+        }
+        // this step's rows; then the next step's state and its columns / weights in flight
+        const int crow = row, ce = e, cee = ee;
+        const float cdiv = div;
+        const bool fin = crow >= 0 && ce + U >= cee;
+        if (fin) row = -1;
+        e = ce + U;
+        assign();
+        load_cw(c, wn);  // c is dead once the record offsets are formed
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool live = lok && crow >= 0 && ce + u < cee;
+            float *a = &acc_g[live ? min(s[u], trash) : trash];
+            *a = __builtin_fmaf(w[u], v[u], *a);  // one rounding, as in the batched walkers
+        }
+        if (fin) {  // group-uniform: this group's row is complete in its copy
+            wave_lds_fence();
+            float *dst = out + (int64_t)crow * D;
+            for (int j = l0 * 4; j < D; j += KG * 4) {
+                float4 a = *reinterpret_cast<float4 *>(&acc_g[j]);
+                *reinterpret_cast<float4 *>(&acc_g[j]) = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (row_div) {
+                    a.x = a.x / cdiv;
+                    a.y = a.y / cdiv;
+                    a.z = a.z / cdiv;
+                    a.w = a.w / cdiv;
+                }
+                if (add) {
+                    const float4 o = *reinterpret_cast<const float4 *>(&dst[j]);
+                    a.x += o.x;
+                    a.y += o.y;
+                    a.z += o.z;
+                    a.w += o.w;
+                }
+                if (nt)
+                    __builtin_nontemporal_store(__builtin_bit_cast(f32x4, a),
+                                                reinterpret_cast<f32x4 *>(&dst[j]));
+                else
+                    *reinterpret_cast<float4 *>(&dst[j]) = a;
+            }
+            wave_lds_fence();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = wn[u];
+    }
+    (void)cn;
+    return next;
+}
+
+template <int KG, int U, bool WIDE, bool EMIT, bool STREAM = false>
 __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES) void spgemm_fwd_kernel(
     const int32_t *__restrict__ row_ptr, const int32_t *__restrict__ col_idx,
     const float *__restrict__ edge_val, const uint8_t *__restrict__ rec, int RS,
@@ -496,12 +630,23 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
     // Rows whose token lies in [d0, d1): this item owns them.  row_ptr of 64 consecutive rows
     // sits one per lane (window from row wb), for the short-row test below.
     int wb = r, rpw = 0;
-    if constexpr (NC > 1 && !WIDE && !EMIT && MAXK_FWD_SHORT > 0)
+    constexpr bool BATCH = NC > 1 && !WIDE && !EMIT && !STREAM && MAXK_FWD_SHORT > 0;
+    if constexpr (BATCH)
         rpw = row_ptr[r + lane <= num_rows ? r + lane : num_rows];
     while (r < num_rows) {
-        const int64_t rb = row_ptr[r];
+        int64_t rb = row_ptr[r];
         if (rb + r >= d1) break;
-        if constexpr (NC > 1 && !WIDE && !EMIT && MAXK_FWD_SHORT > 0) {
+        if constexpr (STREAM) {
+            // every row of at most MAXK_FWD_STREAM edges by the streaming lane groups; a longer
+            // one (or the item's end) stops them, and the wave walks it below
+            r = stream_rows<KG, U>(acc, DS, r, row_ptr, num_rows, d1, col_idx, edge_val, rec, RS,
+                                   row_div, out, D, k, DS - 1, lane, accumulate,
+                                   MAXK_FWD_STREAM, num_e);
+            if (r >= num_rows) break;
+            rb = row_ptr[r];
+            if (rb + r >= d1) break;
+        }
+        if constexpr (BATCH) {
             // Short-row batch: up to NC consecutive rows, each wholly inside the item and at
             // most MAXK_FWD_SHORT edges long, one per lane group, so a wave keeps NC rows'
             // loads in flight instead of walking one short row at a time (Flickr: avg
@@ -558,10 +703,11 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
 }
 
 // Waves of the plain forward one CU holds at once: 7 per SIMD by VGPRs (65-69 VGPRs, the
-// kernel-resource-usage remarks), 4 for the deep-batch kernel (~100), fewer when the LDS copies
-// (NC rows of DS floats per wave) fill the CU's 160 KB first.
-int fwd_resident_waves(int kg, int DS, bool deep) {
-    const int by_vgpr = deep ? 4 * 4 : 7 * 4;
+// kernel-resource-usage remarks), 4 for the deep-batch kernel (~100), 5 for the streaming-rows
+// kernel (~80-87), fewer when the LDS copies (NC rows of DS floats per wave) fill the CU's
+// 160 KB first.
+int fwd_resident_waves(int kg, int DS, int per_simd) {
+    const int by_vgpr = per_simd * 4;
     const size_t per_block = (size_t)kWavesPerBlock * (kWave / kg) * DS * sizeof(float);
     const int by_lds = (int)(kPullLdsBytes / per_block) * kWavesPerBlock;
     return by_lds < by_vgpr ? by_lds : by_vgpr;
@@ -592,6 +738,9 @@ struct FwdLayout {
     // the deep-batch kernel runs: a dense graph (average degree >= kFwdSparseDegree), 32-bit
     // record offsets, no selector stream written (launch_fwd)
     bool deep;
+    // the streaming-rows kernel runs (stream_rows): a sparse graph, 32-bit record offsets,
+    // no selector stream written, D % 4 == 0
+    bool stream;
     size_t rec_off, rec_bytes, slab_off, slab_bytes, row_off, total;
 };
 
@@ -603,9 +752,12 @@ FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, i
     L.RS = record_stride(k, num_cols);
     L.DS = copy_stride(D);
     L.kg = fwd_lanes_per_edge(k, num_rows, num_e);
-    L.deep = !emit && num_e >= kFwdSparseDegree * num_rows && num_cols < (1 << 24) &&
-             (uint64_t)num_cols * (uint64_t)L.RS < (1ull << 32);
-    L.chunk = fwd_chunk(num_rows, num_e, chunk, fwd_resident_waves(L.kg, L.DS, L.deep));
+    const bool narrow = num_cols < (1 << 24) && (uint64_t)num_cols * (uint64_t)L.RS < (1ull << 32);
+    L.deep = !emit && num_e >= kFwdSparseDegree * num_rows && narrow;
+    L.stream = MAXK_FWD_STREAM > 0 && !emit && narrow && L.kg >= 16 && D % 4 == 0 &&
+               num_e < kFwdSparseDegree * num_rows;
+    L.chunk = fwd_chunk(num_rows, num_e, chunk,
+                        fwd_resident_waves(L.kg, L.DS, L.deep ? 4 : L.stream ? 5 : 7));
     const int64_t n = ceil_div(num_rows + num_e, L.chunk);
     L.n_items = (int)(n > 0 ? n : 1);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -635,7 +787,13 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, true>), grid, dim3(kBlock), lds, s,
                            row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
                            num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, esel);
-    else if (L.deep)
+    else if (L.stream) {
+        if constexpr (KG >= 16)
+            hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, false, true>), grid, dim3(kBlock),
+                               lds, s, row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab,
+                               slab_row, num_rows, num_e, D, L.DS, k, L.chunk, L.n_items,
+                               accumulate, nullptr);
+    } else if (L.deep)
         // dense graphs: 16 wave steps of loads per batch (Reddit-sized k = 16 forward 1.613 ->
         // 1.594 ms, k = 32 / 64 and ogbn-proteins 0.3-0.8 % faster; on the sparse products
         // graph, whose rows hold ~50 edges, 16 steps cost occupancy for nothing: 3.23 -> 4.19

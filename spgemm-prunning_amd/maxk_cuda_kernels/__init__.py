@@ -20,6 +20,7 @@ Differences from the reference, all deliberate (DESIGN.md "Boundary"):
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import warnings
@@ -112,7 +113,8 @@ def _validate_call(validate, row_ptr, col_idx, num_cols, sel, D):
 
 
 def _ptr(t: Optional[torch.Tensor]):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() > 0 else None
+    # a plain int: ctypes converts it for the c_void_p argument (no c_void_p object per call)
+    return t.data_ptr() if t is not None and t.numel() > 0 else None
 
 
 def _need(t, name, dtype=None):
@@ -127,7 +129,21 @@ def _need(t, name, dtype=None):
 
 
 def _stream(dev):
-    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    """torch's current HIP stream on `dev` as a raw pointer (int).  The raw accessor skips the
+    torch.cuda.Stream object torch.cuda.current_stream() builds per call (~3 us of the ~20 us
+    a small graph's call spent on the host, tools/host_profile.py)."""
+    return torch._C._cuda_getCurrentRawStream(
+        dev.index if dev.index is not None else torch.cuda.current_device())
+
+
+_NO_SWITCH = contextlib.nullcontext()
+
+
+def _on(dev):
+    """torch.cuda.device(dev), or nothing when dev is already the current device (the
+    context manager costs ~2.6 us per call)."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    return _NO_SWITCH if idx == torch.cuda.current_device() else torch.cuda.device(dev)
 
 
 def _validate_graph(row_ptr, col_idx, num_cols, num_e):
@@ -167,7 +183,7 @@ def build_warp4_metadata(indptr: torch.Tensor, warp_max_nz: int = 64) -> torch.T
     _need(indptr, "indptr", torch.int32)
     dev = indptr.device
     V = indptr.numel() - 1
-    with torch.cuda.device(dev):
+    with _on(dev):
         s = _stream(dev)
         n = ctypes.c_int64(0)
         _capi.check(_lib().maxk_warp4_count(_ptr(indptr), V, warp_max_nz, ctypes.byref(n), s),
@@ -248,7 +264,7 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         if tuple(edge_sel_out.shape) != (E, k):
             raise RuntimeError("edge_sel_out must be [num_e, k]")
         fn = L.maxk_spgemm_forward_accumulate_sel if accumulate else L.maxk_spgemm_forward_sel
-        with torch.cuda.device(dev):
+        with _on(dev):
             _capi.check(fn(
                 _ptr(indptr), _ptr(indices), _ptr(values), _ptr(cbsr_val), _ptr(cbsr_idx),
                 _ptr(row_div), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws),
@@ -256,7 +272,7 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                 "maxk_spgemm_forward_accumulate_sel" if accumulate else "maxk_spgemm_forward_sel")
         return out
     fn = L.maxk_spgemm_forward_accumulate if accumulate else L.maxk_spgemm_forward
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(fn(
             _ptr(indptr), _ptr(indices), _ptr(values), _ptr(cbsr_val), _ptr(cbsr_idx),
             _ptr(row_div), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws), ws.numel(),
@@ -285,7 +301,7 @@ def transpose_plan(indices: torch.Tensor, num_cols: int, cache: bool = True):
     L = _lib()
     ws = torch.empty(max(1, L.maxk_transpose_plan_workspace_size(num_cols, E)), dtype=torch.uint8,
                      device=dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(L.maxk_transpose_plan(_ptr(indices), num_cols, E, _ptr(col_ptr),
                                           _ptr(csc_eid), _ptr(ws), ws.numel(), _stream(dev)),
                     "maxk_transpose_plan")
@@ -325,7 +341,7 @@ def bucket_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True
     bdst = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
     ws = torch.empty(max(1, L.maxk_bucket_plan_workspace_size(num_cols, E)), dtype=torch.uint8,
                      device=dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(L.maxk_bucket_plan(_ptr(indices), num_cols, E, shift, _ptr(bptr), _ptr(beid),
                                        _ptr(bdst), _ptr(ws), ws.numel(), _stream(dev)),
                     "maxk_bucket_plan")
@@ -372,7 +388,7 @@ def bsort_plan(indptr: torch.Tensor, indices: torch.Tensor, num_cols: int, k: in
     wrow = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
     ws = torch.empty(max(1, L.maxk_bsort_plan_workspace_size(num_cols, E)), dtype=torch.uint8,
                      device=dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(L.maxk_bsort_plan(_ptr(indptr), _ptr(indices), num_rows, num_cols, E, int(k),
                                       shift, _ptr(bptr), _ptr(bpos), _ptr(bdst), _ptr(wsrc),
                                       _ptr(wrow), _ptr(ws), ws.numel(), _stream(dev)),
@@ -402,16 +418,19 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     (indptr, indices, values) tensor objects and their version counters -- indptr assigns
     the edges to rows and slices, and the weights are copied into the plan, so a plan serves
     the graph and values it was built from.  `shift` overrides the bucket shift
-    (maxk_pull_shift(k) by default; any shift the C ABI accepts for k)."""
+    (maxk_pull_shift_for by default: maxk_pull_shift(k), smaller on a small graph the one-launch
+    direct form takes, maxk_pull_direct; any shift the C ABI accepts for k)."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32)):
         _need(t, n, dt)
     L = _lib()
-    shift = int(L.maxk_pull_shift(int(k))) if shift is None else int(shift)
+    num_rows = indptr.numel() - 1
+    E = indices.numel()
+    shift = (int(L.maxk_pull_shift_for(num_rows, int(num_cols), E, int(dim), int(k)))
+             if shift is None else int(shift))
     if shift < 0:
         raise RuntimeError(f"pull_plan: invalid k {k}")
-    num_rows = indptr.numel() - 1
-    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(num_cols), int(dim),
+    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(num_cols), E, int(dim),
                                                               int(k)))
     key = (id(indptr), id(indices), id(values), shift, S)
     hit = _PULL_CACHE.get(key)
@@ -428,7 +447,7 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     ent = torch.empty(max(E, 1), 2, dtype=torch.int32, device=dev)[:E]
     ws = torch.empty(max(1, L.maxk_pull_plan_workspace_size(num_rows, num_cols, E, shift, S)),
                      dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(L.maxk_pull_plan(_ptr(indptr), _ptr(indices), _ptr(values), num_rows,
                                      num_cols, E, shift, S, _ptr(tptr), _ptr(ent), _ptr(ws),
                                      ws.numel(), _stream(dev)), "maxk_pull_plan")
@@ -506,7 +525,7 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
     ws = torch.empty(max(1, L.maxk_hybrid_plan_workspace_size(num_rows, num_cols, E, shift, S)),
                      dtype=torch.uint8, device=dev)
     counts = (ctypes.c_int64 * 3)()
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(L.maxk_hybrid_plan(
             _ptr(indptr), _ptr(indices), _ptr(values), _ptr(tptr), _ptr(ent), num_rows, num_cols,
             E, shift, S, float(density), _ptr(tile_list), _ptr(tile_ent), _ptr(bucket_ptr),
@@ -565,7 +584,7 @@ def _scaled_entries(ent: torch.Tensor, tiles: Optional[torch.Tensor], tile_ent: 
     sc = torch.empty_like(ent)
     dev = ent.device
     n_runs = tile_ent.numel() - 1
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(_lib().maxk_pull_entries_scale(
             _ptr(ent), _ptr(tiles), _ptr(tile_ent), n_runs, num_rows, num_cols, shift, S,
             _ptr(row_div), _ptr(sc), _stream(dev)), "maxk_pull_entries_scale")
@@ -600,7 +619,7 @@ def pull_locality(indptr: torch.Tensor, indices: torch.Tensor, shift: int) -> fl
     dev = indices.device
     out = ctypes.c_double(0.0)
     ws = torch.empty(8, dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(_lib().maxk_pull_locality(_ptr(indptr), _ptr(indices), indptr.numel() - 1,
                                               indices.numel(), int(shift), ctypes.byref(out),
                                               _ptr(ws), ws.numel(), _stream(dev)),
@@ -750,7 +769,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         ws_bytes = L.maxk_sspmm_backward_hybrid_workspace_size(num_rows, num_cols, oix.numel(),
                                                                D, k, n_t)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        with torch.cuda.device(dev):
+        with _on(dev):
             overlap = (oix.numel() > 0 and n_t > 0
                        and os.environ.get("MAXK_HYBRID_STREAMS", "1") != "0")
             if not overlap:  # everything on the caller's stream, in one C-ABI call
@@ -797,7 +816,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                 ent, row_div = sc, None
         ws_bytes = L.maxk_sspmm_backward_pull_workspace_size(num_rows, num_cols, D, k, S)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        with torch.cuda.device(dev):
+        with _on(dev):
             _capi.check(L.maxk_sspmm_backward_pull(
                 _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tptr), _ptr(ent), shift,
                 S, _ptr(out), num_rows, num_cols, E, D, k, _ptr(ws), ws.numel(), _stream(dev)),
@@ -807,7 +826,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         bptr, beid, bdst, shift = plan if plan is not None else bucket_plan(indices, num_cols, k)
         ws_bytes = L.maxk_sspmm_backward_bucket_workspace_size(num_rows, num_cols, E, D, k, chunk)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        with torch.cuda.device(dev):
+        with _on(dev):
             _capi.check(L.maxk_sspmm_backward_bucket(
                 _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
                 _ptr(cbsr_idx), _ptr(bptr), _ptr(beid), _ptr(bdst), shift, _ptr(out), num_rows,
@@ -828,7 +847,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                 raise RuntimeError("edge_sel must be [num_e, k]")
         ws_bytes = L.maxk_sspmm_backward_bsort_workspace_size(num_rows, num_cols, E, D, k)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        with torch.cuda.device(dev):
+        with _on(dev):
             _capi.check(L.maxk_sspmm_backward_bsort(
                 _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
                 _ptr(cbsr_idx), _ptr(edge_sel), _ptr(bptr), _ptr(bpos), _ptr(bdst), _ptr(wsrc),
@@ -838,7 +857,7 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     if mode == "atomic":
         ws_bytes = L.maxk_sspmm_backward_workspace_size(num_rows, num_cols, E, D, k, chunk)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        with torch.cuda.device(dev):
+        with _on(dev):
             _capi.check(L.maxk_sspmm_backward(
                 _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
                 _ptr(cbsr_idx), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws),
@@ -851,13 +870,13 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
         _need(edge_sel, "edge_sel", torch.uint8)
         if tuple(edge_sel.shape) != (E, k):
             raise RuntimeError("edge_sel must be [num_e, k]")
-        with torch.cuda.device(dev):
+        with _on(dev):
             _capi.check(L.maxk_sspmm_backward_csc_sel(
                 _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
                 _ptr(edge_sel), _ptr(col_ptr), _ptr(csc_eid), _ptr(out), num_rows, num_cols, E,
                 D, k, chunk, _ptr(ws), ws.numel(), _stream(dev)), "maxk_sspmm_backward_csc_sel")
         return out
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(L.maxk_sspmm_backward_csc(
             _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
             _ptr(cbsr_idx), _ptr(col_ptr), _ptr(csc_eid), _ptr(out), num_rows, num_cols, E, D,
@@ -971,7 +990,7 @@ def topk_cbsr(x: torch.Tensor, k: int, with_int32: bool = False):
     else:
         raise RuntimeError("Input must be float32 or uint8")
     check = _checks_topk_rows(dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(fn(_ptr(x), x.stride(0), _ptr(val), _ptr(idx), _ptr(idx32), V, D, k,
                        _stream(dev)), name)
     if check:
@@ -986,7 +1005,7 @@ def topk_error_rows(device=None, reset: bool = True) -> int:
     inside its own k winner slots."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
     n = ctypes.c_int64(0)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(_lib().maxk_topk_error_rows(ctypes.byref(n), 1 if reset else 0,
                                                 _stream(dev)), "maxk_topk_error_rows")
     return int(n.value)
@@ -1037,7 +1056,7 @@ def cbsr_scatter_dense(cbsr_val: torch.Tensor, cbsr_idx: torch.Tensor, dim_origi
     dev = cbsr_val.device
     if out is None:
         out = torch.empty(V, dim_origin, dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(_lib().maxk_cbsr_scatter_dense(_ptr(cbsr_val), _ptr(cbsr_idx), _ptr(out), V,
                                                    dim_origin, k, _stream(dev)),
                     "maxk_cbsr_scatter_dense")
@@ -1061,7 +1080,7 @@ def topk_cbsr_dense(x: torch.Tensor, k: int):
     idx = torch.empty(V, k, dtype=torch.uint8, device=dev)
     dense = torch.empty(V, D, dtype=torch.float32, device=dev)
     check = _checks_topk_rows(dev)
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(_lib().maxk_topk_cbsr_dense(_ptr(x), x.stride(0), _ptr(val), _ptr(idx),
                                                 _ptr(dense), V, D, k, _stream(dev)),
                     "maxk_topk_cbsr_dense")
@@ -1093,7 +1112,7 @@ def topk_backward(grad_val: Optional[torch.Tensor], grad_dense: Optional[torch.T
         _need(out, "out", torch.float32)
         if tuple(out.shape) != (V, dim_origin):
             raise RuntimeError("out must be [V, dim_origin]")
-    with torch.cuda.device(dev):
+    with _on(dev):
         _capi.check(_lib().maxk_topk_backward(_ptr(grad_val), _ptr(grad_dense), _ptr(cbsr_idx),
                                               _ptr(out), V, dim_origin, k, _stream(dev)),
                     "maxk_topk_backward")

@@ -341,6 +341,28 @@ def test_pull_backward_other_shifts(mk, cuda, k):
         close(gs, ref)
 
 
+@pytest.mark.parametrize("k", [8, 16, 32, 64])
+def test_pull_direct_and_three_launch_forms(mk, cuda, k):
+    """Both forms of the pull against the oracle: a small graph (the one-launch direct form,
+    maxk_pull_direct, with several slices of 16-bit rows and a last partial bucket) and one just
+    past the direct form's edge limit (the selector-table / tile-partial / reduce launches),
+    with hub rows and a divisor."""
+    L = mk._lib()
+    for V, avg, direct in ((70001, 9, True), (9000, 950, False)):
+        rng = np.random.default_rng(V + k)
+        row_ptr, col = rand_graph(rng, V, avg, hubs=((5, min(V, 4000)),), empty=11)
+        E = col.size
+        assert bool(L.maxk_pull_direct(V, V, E, 256, k)) == direct, (V, E)
+        val = rng.random(E, dtype=np.float32)
+        sel = np.stack([rng.choice(256, k, replace=False) for _ in range(V)]).astype(np.uint8)
+        g = rng.standard_normal((V, 256), dtype=np.float32)
+        div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+        gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
+                               T(sel, cuda), row_div=T(div, cuda), mode="pull")
+        ref = O.sspmm_bwd(row_ptr, col, val, g, sel, row_div=div)
+        close(gs, ref)
+
+
 def test_pull_backward_repeats(mk, cuda):
     """fp64 tile sums, slices added in a fixed order: two runs agree to fp32 rounding."""
     z = load_golden(CASES[2])
