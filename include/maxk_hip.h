@@ -311,25 +311,14 @@ int maxk_sspmm_backward_pull_tiles(const float *grad_out, const float *row_div,
  * in CSR order, ent[2*num_e] = one uint32 pair per edge: {row - first row of its slice |
  * (column - first column of its bucket) << 16, bits of edge_val}; bucket_shift in [4, 15]
  * (the backward's 16-B selector copies need 16 | 2^shift * k).  maxk_pull_shift(k) is the
- * bucket shift to use (at least 4); maxk_pull_slices(num_rows, num_cols, num_e, dim_origin,
- * dim_k) the default
+ * bucket shift to use (at least 4); maxk_pull_slices(num_rows, num_cols, dim_origin, dim_k) the
+ * default
  * slice count (about 3.5 MiB of G rows per slice and rank part of k -- at most 3 parts' worth
  * -- at least num_rows/65536, 1..256; when that makes at most 5 rounds of workgroups, one per
  * CU of the current device, over num_cols' buckets, the count in [ceil(S/2), S] with the
- * fewest rounds; num_cols <= 0 means num_rows; for a graph the direct form takes
- * (maxk_pull_direct; num_e >= 0) the fewest slices whose rows fit 16 bits). */
+ * fewest rounds; num_cols <= 0 means num_rows). */
 int maxk_pull_shift(int32_t dim_k);
-/* Small graphs: nonzero when maxk_sspmm_backward_pull runs its one-launch direct form (k % 4
- * == 0, k <= 64, G of at most 64 MiB, few edges): one workgroup per (bucket, part) over every
- * slice, grad_cbsr stored straight from it.  maxk_pull_shift_for is the bucket shift a pull
- * plan of that graph should use (maxk_pull_shift(k), smaller for the direct form so its
- * buckets fill the CUs). */
-int maxk_pull_direct(int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
-                     int32_t dim_k);
-int maxk_pull_shift_for(int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
-                        int32_t dim_k);
-int maxk_pull_slices(int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
-                     int32_t dim_k);
+int maxk_pull_slices(int64_t num_rows, int64_t num_cols, int32_t dim_origin, int32_t dim_k);
 size_t maxk_pull_plan_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e,
                                      int32_t bucket_shift, int32_t slices);
 int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,

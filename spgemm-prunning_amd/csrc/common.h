@@ -107,15 +107,6 @@ __host__ __device__ inline int pull_ks(int kp, int shift) {
 #ifndef MAXK_TOPK_LB  // four-row top-k: bit search from a lower bound of the k-th key
 #define MAXK_TOPK_LB 1
 #endif
-#ifndef MAXK_PULL_DIRECT  // small graphs: the pull in one launch (maxk_pull_direct)
-#define MAXK_PULL_DIRECT 1
-#endif
-#ifndef MAXK_PULL_DIRECT_EDGES  // ... up to this many edges
-#define MAXK_PULL_DIRECT_EDGES (8 << 20)
-#endif
-#ifndef MAXK_PULL_DIRECT_WGS  // ... with buckets sized for this many workgroups per CU
-#define MAXK_PULL_DIRECT_WGS 2
-#endif
 #ifndef MAXK_PULL_SEL4  // pull_sel4_kernel: four selectors per thread (aligned selectors)
 #define MAXK_PULL_SEL4 1
 #endif

@@ -442,6 +442,50 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
     wave_lds_fence();
 }
 
+// Records of the streaming walker: cbsr_pack*_kernel's, value at c*RS + 4l, u16 selector at
+// c*RS + 4k + 2l (a folded duplicate or a selector >= D is stored as 0x100 | s, so
+// min(s, trash) is the LDS column).
+struct PackedSrc {
+    __amdgpu_buffer_rsrc_t rrs;
+    uint32_t vo, so, RS;
+    __device__ __forceinline__ void load(int c, float &v, int &s) const {
+        const uint32_t ro = __umul24((uint32_t)c, RS);
+        v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, (int)(ro + vo), 0, 0));
+        s = __builtin_amdgcn_raw_buffer_load_b16(rrs, (int)(ro + so), 0, 0);
+    }
+    __device__ __forceinline__ int col(int s, int D, int trash) const {
+        (void)D;
+        return min(s, trash);
+    }
+};
+// four consecutive copy columns, zeroed as they are read
+__device__ __forceinline__ float4 acc_take4(float *a) {
+    const float4 x = *reinterpret_cast<float4 *>(a);
+    *reinterpret_cast<float4 *>(a) = make_float4(0.f, 0.f, 0.f, 0.f);
+    return x;
+}
+// dst[j..j+4) = x / div (+ dst), 16-B store (nt: past the caches)
+__device__ __forceinline__ void store_out4(float *dst, float4 a, bool scale, float div, bool add,
+                                           bool nt) {
+    if (scale) {
+        a.x = a.x / div;
+        a.y = a.y / div;
+        a.z = a.z / div;
+        a.w = a.w / div;
+    }
+    if (add) {
+        const float4 o = *reinterpret_cast<const float4 *>(dst);
+        a.x += o.x;
+        a.y += o.y;
+        a.z += o.z;
+        a.w += o.w;
+    }
+    if (nt)
+        __builtin_nontemporal_store(__builtin_bit_cast(f32x4, a), reinterpret_cast<f32x4 *>(dst));
+    else
+        *reinterpret_cast<float4 *>(dst) = a;
+}
+
 // Streaming rows (r05; sparse graphs: KG >= 16, so a lane group covers a D = 64 row with one
 // 16-B access per lane).  Each lane group walks whole rows on its own, U edges per step, and
 // takes the item's next row the step its current one ends, so the wave keeps NC rows in flight
@@ -450,15 +494,16 @@ __device__ __forceinline__ void flush_row(float *acc, int DS, float *__restrict_
 // of loads per U edges, against two in the batched path (columns, then records), which on a
 // small sparse graph -- one round of waves, each a chain of such rounds -- is the whole time.
 // A group flushes its finished row from its own LDS copy (16-B stores).  Rows are taken in
-// order while the next one is owned by the item (token < d1) and has at most lmax edges;
+// order while the next one is owned by the item (token < d1) and has at most lmax edges (the
+// callers pass at most `chunk`: a longer row is split over items, and its pieces past d1 belong
+// to the items holding them);
 // returns the first row not taken (the caller walks a longer one with the whole wave).  Copies
-// are zero on entry and on return.
-template <int KG, int U>
+// are zero on entry and on return.  D % 4 == 0.
+template <int KG, int U, class Src>
 __device__ __forceinline__ int stream_rows(float *acc, int DS, int r,
                                            const int32_t *__restrict__ row_ptr, int num_rows,
                                            int64_t d1, const int32_t *__restrict__ col_idx,
-                                           const float *__restrict__ edge_val,
-                                           const uint8_t *__restrict__ rec, int RS,
+                                           const float *__restrict__ edge_val, const Src &src,
                                            const float *__restrict__ row_div,
                                            float *__restrict__ out, int D, int k, int trash,
                                            int lane, int flags, int lmax, int64_t num_e) {
@@ -466,8 +511,6 @@ __device__ __forceinline__ int stream_rows(float *acc, int DS, int r,
     const int g = lane / KG, l0 = lane % KG;
     float *acc_g = acc + g * DS;
     const bool lok = l0 < k;
-    const uint32_t vo = 4u * (uint32_t)(lok ? l0 : k - 1);
-    const uint32_t so = 4u * (uint32_t)k + 2u * (uint32_t)(lok ? l0 : k - 1);
     const bool add = flags & 1, nt = flags & 2;
     // row_ptr window: rows [wb, wb + 64), one per lane
     int wb = r;
@@ -476,7 +519,6 @@ __device__ __forceinline__ int stream_rows(float *acc, int DS, int r,
     const int64_t span = (num_e - ebase) * 4;
     const auto crs = wave_buffer(col_idx + ebase, (uint32_t)(span < 0xffffffffLL ? span : 0xffffffffLL));
     const auto vrs = wave_buffer(edge_val + ebase, (uint32_t)(span < 0xffffffffLL ? span : 0xffffffffLL));
-    const auto rrs = wave_buffer(rec, 0xffffffffu);  // offsets < num_cols * RS < 2^32
     int next = r;       // the next row to hand out (wave-uniform)
     bool stop = false;  // the next row is not the item's or is too long (wave-uniform)
     int row = -1, e = 0, ee = 0;  // this group's row and its edge range [e, ee)
@@ -517,17 +559,12 @@ __device__ __forceinline__ int stream_rows(float *acc, int DS, int r,
     int c[U];
     float w[U];
     load_cw(c, w);
-    int cn[U];  // placeholder for load_cw's signature: the next columns go straight into c
     float wn[U];
     while (__ballot(row >= 0)) {
         float v[U];
         int s[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t ro = __umul24((uint32_t)c[u], (uint32_t)RS);
-            v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, (int)(ro + vo), 0, 0));
-            s[u] = __builtin_amdgcn_raw_buffer_load_b16(rrs, (int)(ro + so), 0, 0);
-        }
+        for (int u = 0; u < U; ++u) src.load(c[u], v[u], s[u]);
         // this step's rows; then the next step's state and its columns / weights in flight
         const int crow = row, ce = e, cee = ee;
         const float cdiv = div;
@@ -539,40 +576,19 @@ __device__ __forceinline__ int stream_rows(float *acc, int DS, int r,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool live = lok && crow >= 0 && ce + u < cee;
-            float *a = &acc_g[live ? min(s[u], trash) : trash];
+            float *a = &acc_g[live ? src.col(s[u], D, trash) : trash];
             *a = __builtin_fmaf(w[u], v[u], *a);  // one rounding, as in the batched walkers
         }
         if (fin) {  // group-uniform: this group's row is complete in its copy
             wave_lds_fence();
             float *dst = out + (int64_t)crow * D;
-            for (int j = l0 * 4; j < D; j += KG * 4) {
-                float4 a = *reinterpret_cast<float4 *>(&acc_g[j]);
-                *reinterpret_cast<float4 *>(&acc_g[j]) = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (row_div) {
-                    a.x = a.x / cdiv;
-                    a.y = a.y / cdiv;
-                    a.z = a.z / cdiv;
-                    a.w = a.w / cdiv;
-                }
-                if (add) {
-                    const float4 o = *reinterpret_cast<const float4 *>(&dst[j]);
-                    a.x += o.x;
-                    a.y += o.y;
-                    a.z += o.z;
-                    a.w += o.w;
-                }
-                if (nt)
-                    __builtin_nontemporal_store(__builtin_bit_cast(f32x4, a),
-                                                reinterpret_cast<f32x4 *>(&dst[j]));
-                else
-                    *reinterpret_cast<float4 *>(&dst[j]) = a;
-            }
+            for (int j = l0 * 4; j < D; j += KG * 4)
+                store_out4(dst + j, acc_take4(acc_g + j), row_div != nullptr, cdiv, add, nt);
             wave_lds_fence();
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = wn[u];
     }
-    (void)cn;
     return next;
 }
 
@@ -639,9 +655,13 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         if constexpr (STREAM) {
             // every row of at most MAXK_FWD_STREAM edges by the streaming lane groups; a longer
             // one (or the item's end) stops them, and the wave walks it below
-            r = stream_rows<KG, U>(acc, DS, r, row_ptr, num_rows, d1, col_idx, edge_val, rec, RS,
+            const bool lok = lane % KG < k;
+            const uint32_t lc = (uint32_t)(lok ? lane % KG : k - 1);
+            const PackedSrc src{wave_buffer(rec, 0xffffffffu), 4u * lc,
+                                4u * (uint32_t)k + 2u * lc, (uint32_t)RS};
+            r = stream_rows<KG, U>(acc, DS, r, row_ptr, num_rows, d1, col_idx, edge_val, src,
                                    row_div, out, D, k, DS - 1, lane, accumulate,
-                                   MAXK_FWD_STREAM, num_e);
+                                   min(MAXK_FWD_STREAM, chunk), num_e);
             if (r >= num_rows) break;
             rb = row_ptr[r];
             if (rb + r >= d1) break;
@@ -739,7 +759,7 @@ struct FwdLayout {
     // record offsets, no selector stream written (launch_fwd)
     bool deep;
     // the streaming-rows kernel runs (stream_rows): a sparse graph, 32-bit record offsets,
-    // no selector stream written, D % 4 == 0
+    // no selector stream written, D % 4 == 0, k <= 64 (a lane group holds every l)
     bool stream;
     size_t rec_off, rec_bytes, slab_off, slab_bytes, row_off, total;
 };
@@ -754,8 +774,8 @@ FwdLayout fwd_layout(int64_t num_rows, int64_t num_cols, int64_t num_e, int D, i
     L.kg = fwd_lanes_per_edge(k, num_rows, num_e);
     const bool narrow = num_cols < (1 << 24) && (uint64_t)num_cols * (uint64_t)L.RS < (1ull << 32);
     L.deep = !emit && num_e >= kFwdSparseDegree * num_rows && narrow;
-    L.stream = MAXK_FWD_STREAM > 0 && !emit && narrow && L.kg >= 16 && D % 4 == 0 &&
-               num_e < kFwdSparseDegree * num_rows;
+    L.stream = MAXK_FWD_STREAM > 0 && !emit && narrow && L.kg >= 16 && L.kg <= 32 &&
+               D % 4 == 0 && num_e < kFwdSparseDegree * num_rows;
     L.chunk = fwd_chunk(num_rows, num_e, chunk,
                         fwd_resident_waves(L.kg, L.DS, L.deep ? 4 : L.stream ? 5 : 7));
     const int64_t n = ceil_div(num_rows + num_e, L.chunk);

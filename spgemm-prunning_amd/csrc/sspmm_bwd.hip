@@ -1248,102 +1248,19 @@ __device__ __forceinline__ void pull_flush(const double *acc, float *__restrict_
 //  * tiles in XCD order (MAXK_PULL_XCD): XCD x runs the x-th eighth of the tile sequence
 //    in order, so each XCD's L2 holds the one slice it works on instead of every XCD
 //    pulling every slice.
-// Rank of selector s = row[l] among the k selectors of its row, by (selector, l): its position
-// in the ascending order pull_sel_kernel lays the quantile slots out by (row 4-B aligned).
-__device__ __forceinline__ int pull_rank(const uint8_t *__restrict__ row, int k, int l,
-                                         uint32_t s) {
-    int rank = 0;
-    for (int m0 = 0; m0 < k; m0 += 4) {
-        const uint32_t w = *reinterpret_cast<const uint32_t *>(row + m0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t sm = (w >> (8 * j)) & 255u;
-            rank += (sm < s) || (sm == s && m0 + j < l);
-        }
-    }
-    return rank;
-}
-
-// Direct form (r05, small graphs: maxk_pull_direct): one workgroup per (bucket, part) walks the
-// bucket's tile of EVERY slice in turn into one accumulator, so nothing is left to reduce
-// across workgroups: the slot order of its destinations' selectors is computed in the
-// prologue (pull_rank, instead of pull_sel_kernel's table) and the sums go straight to
-// grad_cbsr at their l (instead of tile partials, pull_reduce_kernel and its l map).  One
-// launch instead of three: a small graph's backward is a few microseconds of kernel work per
-// launch plus each launch's fixed cost.  cbsr_idx rows 4-B aligned (k % 4 == 0).
-template <int VPL>
-__device__ __forceinline__ void pull_direct_sel(uint8_t *sel_lds, const uint8_t *__restrict__ sel,
-                                                int64_t c0, int rows, int k, int kp, int h) {
-    const int ql = kp / VPL;
-    for (int i = threadIdx.x; i < rows * k; i += 1024) {
-        const int d = i / k, l = i - d * k;
-        const uint8_t *row = sel + (c0 + d) * k;
-        const uint32_t s = row[l];
-        const int rank = pull_rank(row, k, l, s);
-        if (rank / kp == h) {
-            const int r = rank - h * kp;
-            sel_lds[d * kp + VPL * (r % ql) + r / ql] = (uint8_t)s;
-        }
-    }
-}
-__device__ __forceinline__ void pull_direct_flush(const double *acc, const uint8_t *__restrict__ sel,
-                                                  float *__restrict__ grad_cbsr, int64_t c0,
-                                                  int rows, int k, int kp, int h, int ks,
-                                                  int vpl, bool add) {
-    const int ql = kp / vpl;
-    for (int i = threadIdx.x; i < rows * k; i += 1024) {
-        const int d = i / k, l = i - d * k;
-        const uint8_t *row = sel + (c0 + d) * k;
-        const int rank = pull_rank(row, k, l, row[l]);
-        if (rank / kp == h) {
-            const int r = rank - h * kp;
-            const float v = (float)acc[d * ks + vpl * (r % ql) + r / ql];
-            float *o = grad_cbsr + (c0 + d) * k + l;
-            *o = add ? *o + v : v;
-        }
-    }
-}
-
-template <int LR, int U, bool FULLD, int VPL, bool DIRECT = false>
+template <int LR, int U, bool FULLD, int VPL>
 __global__ __launch_bounds__(1024) void pull_q_kernel(
     const float *__restrict__ Gp, const uint8_t *__restrict__ sel_q,
     const int32_t *__restrict__ tile_ptr, const uint2 *__restrict__ ent,
     float *__restrict__ tile_out, int64_t num_cols, int n_buckets, int n_tiles,
     int rows_per_slice, int64_t num_rows, int D, int k, int kp, int shift,
-    const int32_t *__restrict__ tile_list, int slices = 1, int add = 0) {
+    const int32_t *__restrict__ tile_list) {
     // tile_list (maxk_sspmm_backward_pull_tiles): only the listed tiles run; tile_ptr then
-    // holds their entry ranges and tile_out their partials, both by list position.
-    // DIRECT: sel_q is the caller's cbsr_idx, tile_out is grad_cbsr, one workgroup per
-    // (bucket, part) over all `slices` (see pull_direct_sel)
+    // holds their entry ranges and tile_out their partials, both by list position
     extern __shared__ double acc[];  // [ks << shift], then [kp << shift] selector bytes
     const int tid = threadIdx.x;
     const int ks = pull_ks(kp, shift);
     const int H = k / kp;
-    if constexpr (DIRECT) {
-        const int j = blockIdx.x / H, h = blockIdx.x % H;
-        if (j >= n_buckets) return;
-        const int64_t c0 = (int64_t)j << shift;
-        const int rows = num_cols - c0 < (1 << shift) ? (int)(num_cols - c0) : (1 << shift);
-        uint8_t *sel_lds = reinterpret_cast<uint8_t *>(acc + (ks << shift));
-        for (int i = tid; i < (ks << shift); i += 1024) acc[i] = 0.0;
-        for (int i = tid; i < (kp << shift) / 4; i += 1024)
-            reinterpret_cast<uint32_t *>(sel_lds)[i] = 0u;
-        __syncthreads();
-        pull_direct_sel<VPL>(sel_lds, sel_q, c0, rows, k, kp, h);
-        __syncthreads();
-        for (int sl = 0; sl < slices; ++sl) {
-            const int t = sl * n_buckets + j;
-            const PullTile p = pull_tile_of(t, t, tile_ptr, n_buckets, rows_per_slice, num_rows,
-                                            shift);
-            const auto grs = wave_buffer(Gp + p.r0 * D,
-                                         (uint32_t)(p.nrows > 0 ? p.nrows : 0) * (uint32_t)D * 4u);
-            const auto ers = wave_buffer(ent + p.s0, (uint32_t)(p.s1 - p.s0) * 8u);
-            pull_q_entries<LR, U, FULLD, VPL>(acc, sel_lds, grs, ers, p.s1 - p.s0, D, kp, shift);
-        }
-        __syncthreads();
-        pull_direct_flush(acc, sel_q, tile_out, c0, rows, k, kp, h, ks, VPL, add & 1);
-        return;
-    }
     const int tp = MAXK_PULL_XCD ? xcd_contiguous_block(blockIdx.x, gridDim.x) : blockIdx.x;
     if (tp >= n_tiles * H) return;  // the XCD grid's padding
     const int ti = tp / H, h = tp % H;
@@ -1963,8 +1880,6 @@ extern "C" int maxk_sspmm_backward_bsort(
 
 // ---- pull backward: C entry ------------------------------------------------------------
 namespace maxk {
-inline bool fulld_of(int dim_origin) { return dim_origin == kMaxDim; }
-
 // Parts of pull_q_kernel for k and a plan's bucket shift: the fewest H (k % (4H) == 0) whose
 // accumulator [(k/H + 1) << shift] doubles and selector rows [k/H << shift] bytes fit the
 // LDS; 0 if none does.
@@ -2070,33 +1985,6 @@ int pull_impl(const float *grad_out, const float *row_div, const uint8_t *cbsr_i
         const int vpl = kp != 8 ? 4 : MAXK_PULL_VPL8 ? MAXK_PULL_VPL8 : parts == 1 ? 8 : 4;
         lmap = lm;
         if (!front) goto reduce;
-        if (!listed && back && maxk_pull_direct(num_rows, num_cols, num_e, dim_origin, k) &&
-            (reinterpret_cast<uintptr_t>(cbsr_idx) & 3) == 0) {
-            // small graph: one launch (pull_direct_sel), no selector table, partials or reduce
-            const unsigned grid = (unsigned)(nb * parts);
-            switch (vpl == 2   ? (fulld_of(dim_origin) ? -1 : -2)
-                    : vpl == 8 ? (fulld_of(dim_origin) ? -3 : -4)
-                               : lanes_per_edge(kp / 4) * 2 + (fulld_of(dim_origin) ? 1 : 0)) {
-#define MAXK_CASE_V(CASE, LRV, FD, VP)                                                         \
-    case CASE:                                                                                 \
-        hipLaunchKernelGGL((pull_q_kernel<LRV, MAXK_PULL_QU, FD, VP, true>), dim3(grid),        \
-                           dim3(1024), lds_q, s, Gp, cbsr_idx, tile_ptr, ent2, grad_cbsr,       \
-                           num_cols, (int)nb, (int)tiles, (int)rps, num_rows, dim_origin, k, kp, \
-                           bucket_shift, nullptr, slices, accumulate & 1);                      \
-        break;
-#define MAXK_CASE(LRV) MAXK_CASE_V(LRV * 2 + 1, LRV, true, 4) MAXK_CASE_V(LRV * 2, LRV, false, 4)
-                MAXK_CASE(1) MAXK_CASE(2) MAXK_CASE(4) MAXK_CASE(8) MAXK_CASE(16)
-                MAXK_CASE_V(-1, 4, true, 2) MAXK_CASE_V(-2, 4, false, 2)
-                MAXK_CASE_V(-3, 1, true, 8) MAXK_CASE_V(-4, 1, false, 8)
-#undef MAXK_CASE
-#undef MAXK_CASE_V
-                default:
-                    set_error("unsupported lane group");
-                    return MAXK_ERR_INVALID;
-            }
-            MAXK_LAUNCHED("pull_q_kernel");
-            return MAXK_OK;
-        }
         if (MAXK_PULL_SEL4 && (reinterpret_cast<uintptr_t>(cbsr_idx) & 3) == 0) {
             const int nd4 = kBlock / (k / 4);
             hipLaunchKernelGGL(pull_sel4_kernel, dim3((unsigned)ceil_div(num_cols, nd4)),

@@ -405,37 +405,6 @@ static int64_t device_cus() {
     return n;
 }
 
-namespace maxk {
-int pull_parts(int k, int shift);  // sspmm_bwd.hip
-}
-
-// Small graphs (r05): the pull in one launch (pull_q_kernel's DIRECT form: a workgroup per
-// (bucket, part) walks every slice's tile of its bucket, computes its destinations' slot order
-// itself and stores grad_cbsr directly).  Taken when G stays cache-resident (<= 64 MiB) and the
-// edges are few enough that the three launches' fixed costs are a large share: Flickr-sized
-// (89k rows, D = 64, 1M edges) the quantile-slot pull took 5 + 33 + 4.4 us of kernels plus
-// ~22 us of host launch work per call at k = 16 (r05 session 2, tools/host_profile.py).
-extern "C" int maxk_pull_direct(int64_t num_rows, int64_t num_cols, int64_t num_e,
-                                int32_t dim_origin, int32_t dim_k) {
-    (void)num_cols;
-    return MAXK_PULL_DIRECT && MAXK_PULL_Q && dim_k % 4 == 0 && dim_k <= 64 && num_rows > 0 &&
-           num_e <= (int64_t)MAXK_PULL_DIRECT_EDGES &&
-           (double)num_rows * dim_origin * 4 <= 64.0 * (1 << 20);
-}
-
-// The pull plan's bucket shift for a graph: maxk_pull_shift(k), or on a graph the direct form
-// takes, the largest shift that still gives MAXK_PULL_DIRECT_WGS workgroups per CU (buckets x
-// parts): the direct form has no slices to spread over the CUs, only buckets.
-extern "C" int maxk_pull_shift_for(int64_t num_rows, int64_t num_cols, int64_t num_e,
-                                   int32_t dim_origin, int32_t dim_k) {
-    int s = maxk_pull_shift(dim_k);
-    if (s < 0 || !maxk_pull_direct(num_rows, num_cols, num_e, dim_origin, dim_k)) return s;
-    if (num_cols <= 0) num_cols = num_rows;
-    const int64_t want = (int64_t)MAXK_PULL_DIRECT_WGS * device_cus();
-    while (s > 4 && maxk_bucket_count(num_cols, s) * maxk::pull_parts(dim_k, s) < want) --s;
-    return s;
-}
-
 // ~3.5 MiB of G rows per slice and part: a part gathers only its share of a row's columns
 // (its rank range of the sorted selectors), so an XCD's L2 holds H times the rows of G for
 // it.  The S tile partials (S x num_cols x k floats, written and read once) fall as the
@@ -448,14 +417,10 @@ extern "C" int maxk_pull_shift_for(int64_t num_rows, int64_t num_cols, int64_t n
 // a row's columns, the more rows a slice may hold -- k = 8 (one 8-slot part) best at
 // S = 44 (5.3 MiB; 1.400 ms against 1.418 at S = 66), k = 16 (two 8-slot parts) at S = 28
 // (4.1 MiB per part; 2.120 against 2.145 at S = 33), k = 32 (two 16-slot parts) still at 33.
-extern "C" int maxk_pull_slices(int64_t num_rows, int64_t num_cols, int64_t num_e,
-                                int32_t dim_origin, int32_t dim_k) {
+extern "C" int maxk_pull_slices(int64_t num_rows, int64_t num_cols, int32_t dim_origin,
+                                int32_t dim_k) {
     if (num_rows <= 0 || dim_origin <= 0) return 1;
     if (num_cols <= 0) num_cols = num_rows;
-    // the direct form walks every slice of its bucket in turn, each a pipeline fill and
-    // drain: as few slices as the plan's 16-bit rows allow (num_e < 0: not known, no direct)
-    if (num_e >= 0 && maxk_pull_direct(num_rows, num_cols, num_e, dim_origin, dim_k))
-        return (int)((num_rows + 65535) / 65536);
     const int parts = dim_k % 4 == 0 ? pull_parts_of(dim_k) : 1;
     const int64_t part_bytes = dim_k <= 8    ? maxk::kPullSliceBytes * 3 / 2
                                : dim_k <= 16 ? maxk::kPullSliceBytes * 33 / 28

@@ -194,8 +194,8 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
     (void)row_div_b;
     switch (b.mode) {
         case MAXK_BWD_PULL: {
-            b.shift = maxk_pull_shift_for(V, V, E, D, k);
-            b.slices = maxk_pull_slices(V, V, E, D, k);
+            b.shift = maxk_pull_shift(k);
+            b.slices = maxk_pull_slices(V, V, D, k);
             const int64_t nb = maxk_bucket_count(V, b.shift);
             b.plan_a.alloc((size_t)(b.slices * nb + 1) * 4);
             b.plan_b.alloc((size_t)E * 8);
@@ -212,8 +212,8 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
             return;
         }
         case MAXK_BWD_HYBRID: {
-            b.shift = maxk_pull_shift_for(V, V, E, D, k);
-            b.slices = maxk_pull_slices(V, V, E, D, k);
+            b.shift = maxk_pull_shift(k);
+            b.slices = maxk_pull_slices(V, V, D, k);
             const int64_t nb = maxk_bucket_count(V, b.shift), nt = b.slices * nb;
             Buf tptr((size_t)(nt + 1) * 4), ent((size_t)E * 8);
             {

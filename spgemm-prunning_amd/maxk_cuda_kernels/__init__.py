@@ -418,19 +418,16 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     (indptr, indices, values) tensor objects and their version counters -- indptr assigns
     the edges to rows and slices, and the weights are copied into the plan, so a plan serves
     the graph and values it was built from.  `shift` overrides the bucket shift
-    (maxk_pull_shift_for by default: maxk_pull_shift(k), smaller on a small graph the one-launch
-    direct form takes, maxk_pull_direct; any shift the C ABI accepts for k)."""
+    (maxk_pull_shift(k) by default; any shift the C ABI accepts for k)."""
     for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
                      (values, "values", torch.float32)):
         _need(t, n, dt)
     L = _lib()
     num_rows = indptr.numel() - 1
-    E = indices.numel()
-    shift = (int(L.maxk_pull_shift_for(num_rows, int(num_cols), E, int(dim), int(k)))
-             if shift is None else int(shift))
+    shift = int(L.maxk_pull_shift(int(k))) if shift is None else int(shift)
     if shift < 0:
         raise RuntimeError(f"pull_plan: invalid k {k}")
-    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(num_cols), E, int(dim),
+    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(num_cols), int(dim),
                                                               int(k)))
     key = (id(indptr), id(indices), id(values), shift, S)
     hit = _PULL_CACHE.get(key)

@@ -76,9 +76,7 @@ SIGNATURES = {
                                                       _i32, _i32, _p, _i64, _i64, _i64, _i32,
                                                       _i32, _p, _sz, _p]),
     "maxk_pull_shift": (ctypes.c_int, [_i32]),
-    "maxk_pull_direct": (ctypes.c_int, [_i64, _i64, _i64, _i32, _i32]),
-    "maxk_pull_shift_for": (ctypes.c_int, [_i64, _i64, _i64, _i32, _i32]),
-    "maxk_pull_slices": (ctypes.c_int, [_i64, _i64, _i64, _i32, _i32]),
+    "maxk_pull_slices": (ctypes.c_int, [_i64, _i64, _i32, _i32]),
     "maxk_pull_plan_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32]),
     "maxk_pull_plan": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _sz,
                                       _p]),

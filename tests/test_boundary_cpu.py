@@ -235,23 +235,23 @@ def test_pull_slice_rule():
     buckets, k] per slice."""
     from maxk_cuda_kernels import _capi
     L = _capi.load()
-    assert L.maxk_pull_slices(232965, 0, -1, 256, 16) == 28  # Reddit: 238.6 MB of G rows, 2 parts
-    assert L.maxk_pull_slices(232965, 0, -1, 256, 8) == 44   # 1 part
-    assert L.maxk_pull_slices(232965, 0, -1, 256, 32) == 33  # 2 parts
-    assert L.maxk_pull_slices(232965, 0, -1, 256, 64) == 22  # 4 parts, factor capped at 3
-    assert L.maxk_pull_slices(29121, 0, -1, 256, 16) == 4    # one of 8 row shards
-    assert L.maxk_pull_slices(1, 0, -1, 256, 16) == 1 and L.maxk_pull_slices(0, 0, -1, 256, 16) == 1
-    assert L.maxk_pull_slices(100_000_000, 0, -1, 256, 16) == 256
-    assert L.maxk_pull_slices(2_449_029, 0, -1, 256, 64) == 228
-    assert L.maxk_pull_slices(4_000_000, 0, -1, 16, 64) == 62  # rows in a slice stay <= 65536
+    assert L.maxk_pull_slices(232965, 0, 256, 16) == 28  # Reddit: 238.6 MB of G rows, 2 parts
+    assert L.maxk_pull_slices(232965, 0, 256, 8) == 44   # 1 part
+    assert L.maxk_pull_slices(232965, 0, 256, 32) == 33  # 2 parts
+    assert L.maxk_pull_slices(232965, 0, 256, 64) == 22  # 4 parts, factor capped at 3
+    assert L.maxk_pull_slices(29121, 0, 256, 16) == 4    # one of 8 row shards
+    assert L.maxk_pull_slices(1, 0, 256, 16) == 1 and L.maxk_pull_slices(0, 0, 256, 16) == 1
+    assert L.maxk_pull_slices(100_000_000, 0, 256, 16) == 256
+    assert L.maxk_pull_slices(2_449_029, 0, 256, 64) == 228
+    assert L.maxk_pull_slices(4_000_000, 0, 16, 64) == 62  # rows in a slice stay <= 65536
     # Flickr-sized (89k rows, D = 64): 132 / 352 / 264 tiles at k = 16 / 32 / 64 would leave
     # a nearly empty last round of workgroups; the slices drop to 2 (k = 8 keeps 5: 220, one round)
-    assert [L.maxk_pull_slices(89250, 0, -1, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
-    assert [L.maxk_pull_slices(89250, 89250, -1, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
+    assert [L.maxk_pull_slices(89250, 0, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
+    assert [L.maxk_pull_slices(89250, 89250, 64, k) for k in (8, 16, 32, 64)] == [5, 2, 2, 2]
     # a rectangular shard (a quarter of the rows, every column): rounds counted over the
     # columns' buckets, not the rows'
-    assert L.maxk_pull_slices(44625, 0, -1, 256, 8) == 9
-    assert L.maxk_pull_slices(44625, 89250, -1, 256, 8) == 5
+    assert L.maxk_pull_slices(44625, 0, 256, 8) == 9
+    assert L.maxk_pull_slices(44625, 89250, 256, 8) == 5
     gp = (232965 * 256 * 4 + 255) // 256 * 256
     selq = 2 * ((232965 * 16 + 255) // 256 * 256)  # slot-ordered selectors + their l map
     assert L.maxk_sspmm_backward_pull_workspace_size(232965, 232965, 256, 16, 65) == \
@@ -339,24 +339,3 @@ def test_bench_binding_roofline_and_traffic_order():
     b = bench.binding_roofline(1.0, 1e9, None)
     assert b["bound"] == "hbm_compulsory" and b["frac"] == 0.125
 
-
-def test_pull_direct_rule():
-    """The one-launch pull (maxk_pull_direct) on small graphs only: Flickr-sized (D = 64, 1M
-    edges) takes it, with buckets shrunk until they give one or more workgroups per CU and the
-    fewest slices whose rows fit 16 bits; Reddit- and products-sized graphs keep the
-    three-launch form, the k rule's shift and the L2 slice rule."""
-    from maxk_cuda_kernels import _capi
-    L = _capi.load()
-    for k in (8, 16, 32, 64):
-        assert L.maxk_pull_direct(89250, 89250, 989006, 64, k)
-        s = L.maxk_pull_shift_for(89250, 89250, 989006, 64, k)
-        assert 4 <= s < L.maxk_pull_shift(k)
-        assert L.maxk_bucket_count(89250, s) >= 256
-        assert L.maxk_pull_slices(89250, 89250, 989006, 64, k) == 2  # 89,250 rows > 65,536
-        for V, E in ((232965, 114615891), (2449029, 123718279)):
-            assert not L.maxk_pull_direct(V, V, E, 256, k)
-            assert L.maxk_pull_shift_for(V, V, E, 256, k) == L.maxk_pull_shift(k)
-            assert L.maxk_pull_slices(V, V, E, 256, k) == L.maxk_pull_slices(V, V, -1, 256, k)
-    assert not L.maxk_pull_direct(89250, 89250, 989006, 64, 96)  # k > 64
-    assert not L.maxk_pull_direct(89250, 89250, 989006, 64, 10)  # k % 4 != 0
-    assert not L.maxk_pull_direct(300000, 300000, 1000000, 256, 16)  # G past 64 MiB

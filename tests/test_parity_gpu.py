@@ -341,28 +341,6 @@ def test_pull_backward_other_shifts(mk, cuda, k):
         close(gs, ref)
 
 
-@pytest.mark.parametrize("k", [8, 16, 32, 64])
-def test_pull_direct_and_three_launch_forms(mk, cuda, k):
-    """Both forms of the pull against the oracle: a small graph (the one-launch direct form,
-    maxk_pull_direct, with several slices of 16-bit rows and a last partial bucket) and one just
-    past the direct form's edge limit (the selector-table / tile-partial / reduce launches),
-    with hub rows and a divisor."""
-    L = mk._lib()
-    for V, avg, direct in ((70001, 9, True), (9000, 950, False)):
-        rng = np.random.default_rng(V + k)
-        row_ptr, col = rand_graph(rng, V, avg, hubs=((5, min(V, 4000)),), empty=11)
-        E = col.size
-        assert bool(L.maxk_pull_direct(V, V, E, 256, k)) == direct, (V, E)
-        val = rng.random(E, dtype=np.float32)
-        sel = np.stack([rng.choice(256, k, replace=False) for _ in range(V)]).astype(np.uint8)
-        g = rng.standard_normal((V, 256), dtype=np.float32)
-        div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-        gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
-                               T(sel, cuda), row_div=T(div, cuda), mode="pull")
-        ref = O.sspmm_bwd(row_ptr, col, val, g, sel, row_div=div)
-        close(gs, ref)
-
-
 def test_pull_backward_repeats(mk, cuda):
     """fp64 tile sums, slices added in a fixed order: two runs agree to fp32 rounding."""
     z = load_golden(CASES[2])
@@ -781,6 +759,38 @@ def test_duplicate_selectors_accumulate(mk, cuda):
     y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=17)
     close(y, yo)
     close(gs, go)
+
+
+@pytest.mark.parametrize("D,k", [(64, 16), (64, 64), (128, 32), (128, 8), (256, 16)])
+def test_forward_small_sparse_paths(mk, cuda, D, k):
+    """The small sparse graphs' forwards (r05): the pack-free kernel (D <= 128, fp64 LDS
+    copies over the caller's CBSR) and the streaming rows over packed records (D = 256), with
+    repeated selectors, selectors >= D, empty rows, hub rows split over items (chunk 40) and
+    rows past the streaming limit, against the oracle; the full-width oracle cut back to D is
+    the reference for selectors past D (they contribute nothing)."""
+    rng = np.random.default_rng(D * 100 + k)
+    V = 3000
+    row_ptr, col = rand_graph(rng, V, 9, hubs=((7, 900), (11, 70), (1500, 130)), empty=40)
+    val = rng.random(col.size, dtype=np.float32)
+    cv = rng.standard_normal((V, k)).astype(np.float32)
+    ci = np.stack([rng.choice(D, k, replace=False) for _ in range(V)]).astype(np.uint8)
+    ci[rng.choice(V, 50, replace=False), 0] = ci[rng.choice(V, 50, replace=False), 1]
+    dup = rng.choice(V, 60, replace=False)
+    ci[dup, -1] = ci[dup, 0]                      # repeated selectors sum
+    past = rng.choice(V, 60, replace=False)
+    if D < 256:
+        ci[past, 1] = rng.integers(D, 256, 60).astype(np.uint8)  # contribute nothing
+    div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+    yo = O.spgemm_fwd(row_ptr, col, val, cv, ci, 256, row_div=div)[:, :D]
+    for chunk in (0, 40):
+        y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda),
+                              T(ci, cuda), D, row_div=T(div, cuda), chunk=chunk, validate=False)
+        close(y, yo)
+        acc = torch.ones(V, D, device=cuda)
+        mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda),
+                          T(ci, cuda), D, row_div=T(div, cuda), chunk=chunk, validate=False,
+                          out=acc, accumulate=True)
+        close(acc, yo + 1.0)
 
 
 @pytest.mark.parametrize("k", [4, 12, 16, 32])
