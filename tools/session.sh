@@ -233,6 +233,25 @@ step_kt() {
     --k 8 16 32 64 --json > $O/kernel_test/flickr.txt 2> $O/kernel_test/flickr.err
   python tools/kt_table.py $O/kernel_test
 }
+# the compiled C-ABI consumer (bin/maxk_kernel_test: kernels/main.cu's recipe and wall-clock
+# timing, no Python on the timed path) on the synthetic graphs written as .indptr/.indices to
+# the box's /tmp (r05: the reference's kernel numbers come from that C++ program)
+step_ktc() {
+  mkdir -p $O/kernel_test_cpp
+  local g D
+  for g in flickr reddit products proteins; do
+    D=256; [ $g = flickr ] && D=64
+    timeout -k 10 300 python -c "
+import sys; sys.path.insert(0, 'spgemm-prunning_amd')
+import torch, maxk_graph
+rp, col = maxk_graph.synthetic_graph('$g', device=torch.device('cuda'))
+maxk_graph.save_graph(rp, col, '/tmp/maxk_graphs', '$g')"
+    timeout -k 10 300 spgemm-prunning_amd/bin/maxk_kernel_test $g --dir /tmp/maxk_graphs \
+      --dim $D --k 8,16,32,64 --runs 20 > $O/kernel_test_cpp/$g.txt 2> $O/kernel_test_cpp/$g.err
+    rm -f /tmp/maxk_graphs/$g.indptr /tmp/maxk_graphs/$g.indices
+  done
+  cat $O/kernel_test_cpp/*.txt
+}
 step_epochs() {
   mkdir -p $O/train
   for cfg in "products products" "reddit reddit" "products_comm_ordered products_comm --reorder"; do
@@ -286,6 +305,10 @@ step_collect() {
     mkdir -p $P/kernel_test
     cp $O/kernel_test/*.txt $P/kernel_test/
     python tools/kt_table.py $P/kernel_test > $P/kernel_test_table.md
+  fi
+  if [ -d $O/kernel_test_cpp ]; then
+    mkdir -p $P/kernel_test_cpp
+    cp $O/kernel_test_cpp/*.txt $P/kernel_test_cpp/
   fi
   if [ -d $O/train ]; then
     mkdir -p $P/train
