@@ -327,20 +327,53 @@ int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *
                    size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Dense route (r05): wide top-k, dim_k >= dim_origin / 2 at dim_origin % 4 == 0,
+ * dim_origin <= 128 (MAXK_DENSE_DMAX), dim_k % 4 == 0.  A CBSR row then carries as many bytes as
+ * the dense row, so both directions aggregate dense rows.  Replaces the same reference kernels
+ * as maxk_spgemm_forward / maxk_sspmm_backward (spmm_maxk.cu:17-106,
+ * spmm_maxk_backward.cu:15-121) for those widths; results within fp32 rounding of them.
+ *
+ * maxk_dense_route: 1 when (dim_origin, dim_k) takes the route.  maxk_spgemm_forward takes it
+ *   by itself there (16-B aligned cbsr_val and out, 4-B aligned cbsr_idx; not the _sel forms):
+ *   the CBSR scattered into a dense [num_cols, dim_origin] table in the workspace, then one
+ *   dense row walk (maxk_spgemm_forward_workspace_size covers it).
+ * maxk_dense_plan: the graph's transpose with source rows -- for every CSC slot t of
+ *   maxk_transpose_plan (col_ptr, csc_eid), t_src[t] = the CSR row holding edge csc_eid[t] and
+ *   t_w[t] = edge_val[csc_eid[t]] (int32 / float [num_e]).  Once per graph and weights.
+ * maxk_sspmm_backward_dense: grad_cbsr[c, l] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]] from
+ *   the transpose plan: Y = A^T diag(1/row_div) G walked over dense G rows into the workspace,
+ *   then the k selected columns of each row (selectors >= dim_origin read 0).  Bitwise
+ *   repeatable.  16-B aligned grad_out and grad_cbsr, 4-B aligned cbsr_idx.
+ * ------------------------------------------------------------------------- */
+int maxk_dense_route(int32_t dim_origin, int32_t dim_k);
+int maxk_dense_plan(const int32_t *row_ptr, const float *edge_val, const int32_t *csc_eid,
+                    int64_t num_rows, int64_t num_e, int32_t *t_src, float *t_w, void *stream);
+size_t maxk_sspmm_backward_dense_workspace_size(int64_t num_rows, int64_t num_cols,
+                                                int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                                                int32_t chunk_edges);
+int maxk_sspmm_backward_dense(const int32_t *col_ptr, const int32_t *t_src, const float *t_w,
+                              const float *grad_out, const float *row_div,
+                              const uint8_t *cbsr_idx, float *grad_cbsr, int64_t num_rows,
+                              int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
+                              int32_t chunk_edges, void *workspace, size_t workspace_bytes,
+                              void *stream);
+
+/* ---------------------------------------------------------------------------
  * Hybrid backward and the "auto" backward rule through the C ABI (the Python binding's
  * hybrid_plan / pull_locality / _bwd_mode / _scaled_entries, maxk_cuda_kernels/__init__.py,
  * rest on these).  Replaces the same reference kernels as maxk_sspmm_backward
  * (spmm_maxk_backward.cu:15-121, launched by cuda_kernel_wrappers.cu:58-76).
  *
  * maxk_backward_mode_auto: the backward a graph should use (pure host arithmetic):
- *   MAXK_BWD_PULL where dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and the graph has at
+ *   MAXK_BWD_DENSE where maxk_dense_route(dim_origin, dim_k); else MAXK_BWD_PULL where dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and the graph has at
  *   least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(dim_k) columns) or a G of at
  *   most 64 MiB; else MAXK_BWD_BUCKET on such a dense graph at dim_k <= 16; else MAXK_BWD_HYBRID
  *   when pull_locality (maxk_pull_locality at maxk_pull_shift(dim_k); < 0 = unknown) reaches
  *   MAXK_HYBRID_LOCALITY and dim_k % 4 == 0; else MAXK_BWD_BSORT at dim_k % 4 == 0,
  *   dim_k <= MAXK_BSORT_KMAX when a window of maxk_bsort_window(dim_k) edges holds at least 2
  *   rows per destination bucket on average (W * 2^maxk_bucket_shift(dim_k) >= 2 * num_cols;
- *   ogbn-products k = 8: 4.3); else MAXK_BWD_CSC.  Only csc is bitwise repeatable.
+ *   ogbn-products k = 8: 4.3); else MAXK_BWD_CSC.  Only csc and dense are bitwise
+ *   repeatable.
  * maxk_pull_locality (synchronous): num_e / occupied (source row, bucket of 2^bucket_shift
  *   columns) pairs, columns sorted within rows; workspace >= 8 bytes.
  * maxk_hybrid_plan (synchronous): from the graph's pull plan (maxk_pull_plan with bucket_shift,
@@ -365,6 +398,7 @@ int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *
 #define MAXK_BWD_HYBRID 3
 #define MAXK_BWD_ATOMIC 4
 #define MAXK_BWD_BSORT 5
+#define MAXK_BWD_DENSE 6
 #define MAXK_BSORT_KMAX 8
 #define MAXK_HYBRID_LOCALITY 1.5
 #define MAXK_HYBRID_DENSITY 0.5f

@@ -162,6 +162,18 @@ constexpr size_t kInfinityCacheBytes = 256ull << 20;  // MI355X MALL (MI355X_MIC
 #ifndef MAXK_BSORT_U  // window-sorted phase 1: wave instructions of edges per batch
 #define MAXK_BSORT_U 2
 #endif
+#ifndef MAXK_DENSE_ROUTE  // k >= D / 2: aggregate dense rows (dense_route.hip); 0 = off
+#define MAXK_DENSE_ROUTE 1
+#endif
+#ifndef MAXK_DENSE_DMAX  // the dense route's largest D
+#define MAXK_DENSE_DMAX 128
+#endif
+#ifndef MAXK_DENSE_U  // dense_rows_kernel: edges per lane-group step (Flickr-sized D = 64,
+#define MAXK_DENSE_U 4  // k = 64: 0.094 ms at 8, 0.070 at 4)
+#endif
+#ifndef MAXK_DENSE_WAVES  // dense_rows_kernel: resident waves per CU its item size assumes
+#define MAXK_DENSE_WAVES 24
+#endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
 #endif
@@ -217,6 +229,16 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // stale values from the second replay on (tools/capture_probe*.py).
 __global__ void zero_words_kernel(uint32_t *__restrict__ p, int64_t n);
 int zero_words(void *p, int64_t n, hipStream_t s);
+
+// Dense route (dense_route.hip): whether (D, k) takes it, and the forward through it
+bool dense_route(int D, int k);
+size_t dense_forward_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e, int D,
+                                    int chunk);
+int dense_forward(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
+                  const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div,
+                  float *out, int64_t num_rows, int64_t num_cols, int64_t num_e, int D, int k,
+                  int chunk, void *workspace, size_t workspace_bytes, hipStream_t s,
+                  int accumulate);
 
 // The hardware hands workgroup b to XCD b % 8 (each XCD has its own L2).  With
 // grid = 8 * per, logical block (b % 8) * per + b / 8 makes XCD x run the contiguous

@@ -369,6 +369,7 @@ extern "C" int maxk_pull_entries_scale(const uint32_t *ent, const int32_t *tile_
 extern "C" int maxk_backward_mode_auto(int64_t num_rows, int64_t num_cols, int64_t num_e,
                                        int32_t dim_origin, int32_t dim_k, double pull_locality) {
     const int k = dim_k;
+    if (k > 0 && num_cols > 0 && dim_origin > 0 && dense_route(dim_origin, k)) return MAXK_BWD_DENSE;
     if (k <= 0 || num_cols <= 0 || (dim_origin > 0 && dim_origin % 4 != 0) || !(k % 4 == 0 || k <= 64))
         return MAXK_BWD_CSC;
     const int shift = maxk_bucket_shift(k);

@@ -844,7 +844,11 @@ extern "C" size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t n
     const size_t a = fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges).total;
     const size_t b =
         fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, true).total;
-    return a > b ? a : b;
+    const size_t c = dense_route(dim_origin, dim_k)
+                         ? dense_forward_workspace_size(num_rows, num_cols, num_e, dim_origin,
+                                                        chunk_edges)
+                         : 0;
+    return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
 namespace {
@@ -868,6 +872,14 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
     MAXK_REQUIRE(num_e == 0 || (col_idx && edge_val && cbsr_val && cbsr_idx),
                  "CSR/CBSR pointers must not be NULL");
     MAXK_REQUIRE(num_e == 0 || num_cols > 0, "edges present but num_cols == 0");
+    if (!esel && dense_route(dim_origin, dim_k) && ((uintptr_t)cbsr_val & 15) == 0 &&
+        ((uintptr_t)cbsr_idx & 3) == 0 && ((uintptr_t)out & 15) == 0) {
+        // k >= D / 2: dense rows carry no more bytes than the CBSR (dense_route.hip)
+        MAXK_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-B aligned");
+        return dense_forward(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out,
+                             num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
+                             workspace_bytes, as_stream(stream), accumulate);
+    }
     const FwdLayout L =
         fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges, esel != nullptr);
     MAXK_REQUIRE(workspace && workspace_bytes >= L.total,

@@ -157,6 +157,7 @@ const char *mode_name(int m) {
         case MAXK_BWD_HYBRID: return "hybrid";
         case MAXK_BWD_ATOMIC: return "atomic";
         case MAXK_BWD_BSORT: return "bsort";
+        case MAXK_BWD_DENSE: return "dense";
     }
     return "?";
 }
@@ -168,6 +169,7 @@ int mode_of(const std::string &s) {
     if (s == "hybrid") return MAXK_BWD_HYBRID;
     if (s == "atomic") return MAXK_BWD_ATOMIC;
     if (s == "bsort") return MAXK_BWD_BSORT;
+    if (s == "dense") return MAXK_BWD_DENSE;
     return -1;
 }
 
@@ -297,6 +299,27 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
                     rp, ci, ev, G, row_div, S, nullptr, b.plan_a.as<int32_t>(),
                     b.plan_b.as<int32_t>(), b.plan_c.as<uint16_t>(), b.plan_d.as<uint16_t>(),
                     b.plan_e.as<int32_t>(), b.shift, out, V, V, E, D, k, b.ws.p, b.ws.n, nullptr));
+            };
+            return;
+        }
+        case MAXK_BWD_DENSE: {  // k >= D / 2: dense G rows along the transpose
+            b.plan_a.alloc((size_t)(V + 1) * 4);
+            b.plan_b.alloc((size_t)E * 4);
+            b.plan_c.alloc((size_t)E * 4);
+            b.plan_d.alloc((size_t)E * 4);
+            {
+                Buf tws(maxk_transpose_plan_workspace_size(V, E));
+                MAXK_CHECK(maxk_transpose_plan(ci, V, E, b.plan_a.as<int32_t>(),
+                                               b.plan_b.as<int32_t>(), tws.p, tws.n, nullptr));
+                MAXK_CHECK(maxk_dense_plan(rp, ev, b.plan_b.as<int32_t>(), V, E,
+                                           b.plan_c.as<int32_t>(), b.plan_d.as<float>(), nullptr));
+                HIP_CHECK(hipDeviceSynchronize());
+            }
+            b.ws.alloc(maxk_sspmm_backward_dense_workspace_size(V, V, E, D, k, 0));
+            b.run = [&b, G, row_div, S, out, V, E, D, k] {
+                MAXK_CHECK(maxk_sspmm_backward_dense(b.plan_a.as<int32_t>(), b.plan_c.as<int32_t>(),
+                                                     b.plan_d.as<float>(), G, row_div, S, out, V,
+                                                     V, E, D, k, 0, b.ws.p, b.ws.n, nullptr));
             };
             return;
         }
@@ -526,7 +549,7 @@ int main(int argc, char **argv) {
         else if (a == "--lib-runs") o.lib_runs = std::atoi(next().c_str());
         else if (a == "-h" || a == "--help") {
             std::printf("usage: %s [graph] [--dir DIR] [--k 16,32,64] [--dim 256] "
-                        "[--bwd auto|pull|csc|hybrid|bucket|bsort|atomic] [--check] [--runs 4] "
+                        "[--bwd auto|pull|csc|hybrid|bucket|bsort|atomic|dense] [--check] [--runs 4] "
                         "[--inputs DIR] [--dump DIR]\n", argv[0]);
             return 0;
         } else if (!a.empty() && a[0] != '-') o.graph = a;

@@ -313,6 +313,44 @@ def transpose_plan(indices: torch.Tensor, num_cols: int, cache: bool = True):
     return plan
 
 
+_DENSE_CACHE: "dict" = {}
+
+
+def dense_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, num_cols: int,
+               cache: bool = True):
+    """(col_ptr int32 [num_cols+1], t_src int32 [E], t_w float [E]) of the dense backward: the
+    graph's transpose (transpose_plan) with, per CSC slot, the CSR row of its edge and its
+    weight (maxk_dense_plan).  Cached per (indptr, indices, values) tensor objects and their
+    version counters."""
+    for t, n, dt in ((indptr, "indptr", torch.int32), (indices, "indices", torch.int32),
+                     (values, "values", torch.float32)):
+        _need(t, n, dt)
+    key = (id(indptr), id(indices), id(values))
+    hit = _DENSE_CACHE.get(key)
+    if cache and hit is not None:
+        rp, ri, rv, nc, pv, vi, vv, plan = hit
+        if (rp() is indptr and ri() is indices and rv() is values and nc == num_cols
+                and pv == _ver(indptr) and vi == _ver(indices) and vv == _ver(values)):
+            return plan
+    col_ptr, csc_eid = transpose_plan(indices, num_cols, cache=False)
+    dev = indices.device
+    E = indices.numel()
+    t_src = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
+    t_w = torch.empty(max(E, 1), dtype=torch.float32, device=dev)[:E]
+    with _on(dev):
+        _capi.check(_lib().maxk_dense_plan(_ptr(indptr), _ptr(values), _ptr(csc_eid),
+                                           indptr.numel() - 1, E, _ptr(t_src), _ptr(t_w),
+                                           _stream(dev)), "maxk_dense_plan")
+    plan = (col_ptr, t_src, t_w)
+    if cache:
+        if key not in _DENSE_CACHE:
+            for t in (indptr, indices, values):
+                weakref.finalize(t, _DENSE_CACHE.pop, key, None)
+        _DENSE_CACHE[key] = (weakref.ref(indptr), weakref.ref(indices), weakref.ref(values),
+                             int(num_cols), _ver(indptr), _ver(indices), _ver(values), plan)
+    return plan
+
+
 _BUCKET_CACHE: "dict" = {}
 
 
@@ -463,7 +501,8 @@ _HYBRID_CACHE: "dict" = {}
 MAXK_PULL_NO_REDUCE, MAXK_PULL_REDUCE_ONLY = 2, 4  # include/maxk_hip.h
 MAXK_HYBRID_PRESCALED = 1
 # maxk_backward_mode_auto's codes (include/maxk_hip.h MAXK_BWD_*)
-_MODE_OF_CODE = {0: "pull", 1: "csc", 2: "bucket", 3: "hybrid", 4: "atomic", 5: "bsort"}
+_MODE_OF_CODE = {0: "pull", 1: "csc", 2: "bucket", 3: "hybrid", 4: "atomic", 5: "bsort",
+                 6: "dense"}
 _SIDE: "dict" = {}
 
 
@@ -547,7 +586,7 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
     return plan
 
 
-BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid", "bsort")
+BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid", "bsort", "dense")
 BSORT_KMAX = 8  # MAXK_BSORT_KMAX: the auto rule's bsort limit
 _BSORT_WARNED: set = set()  # (id(indptr), k) already warned about
 
@@ -633,7 +672,9 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
               num_rows: Optional[int] = None, dim: Optional[int] = None,
               graph: Optional[tuple] = None) -> str:
     """Resolve the backward mode.  "auto" (default; MAXK_BWD_MODE overrides) is the C ABI's
-    rule, maxk_backward_mode_auto: "pull" where it measured faster than "csc" -- k % 4 == 0
+    rule, maxk_backward_mode_auto: "dense" at k >= dim / 2 (dim % 4 == 0, dim <= 128, k % 4 ==
+    0: Flickr-shaped D = 64 at k = 32 / 64, where a CBSR row is as wide as the dense row);
+    else "pull" where it measured faster than "csc" -- k % 4 == 0
     or k <= 64, dim % 4 == 0 when dim is given, and at least ~1/2 edge per (source row,
     bucket of 2^maxk_bucket_shift(k) columns) on average (Reddit k=16: 2.2, k=64: 0.54;
     ogbn-proteins k=64: 1.2; ogbn-products: 0.02), or a gradient G of at most 64 MiB (Flickr:
@@ -667,6 +708,9 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
         raise RuntimeError(f"backward mode 'pull' needs k % 4 == 0 or k <= 64, got k={k}")
     if mode == "pull" and dim is not None and dim % 4 != 0:
         raise RuntimeError(f"backward mode 'pull' needs dim_origin % 4 == 0, got {dim}")
+    if mode == "dense" and (k % 4 != 0 or (dim is not None and dim % 4 != 0)):
+        raise RuntimeError(f"backward mode 'dense' needs k % 4 == 0 and dim_origin % 4 == 0, "
+                           f"got k={k}, dim={dim}")
     if mode == "hybrid" and (k % 4 != 0 or (dim is not None and dim % 4 != 0)):
         raise RuntimeError(f"backward mode 'hybrid' needs k % 4 == 0 and dim_origin % 4 == 0, "
                            f"got k={k}, dim={dim}")
@@ -687,6 +731,10 @@ def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[s
         if mode == "hybrid":
             return hybrid_plan(indptr, indices, values, num_cols, k, dim or 256)
         return pull_plan(indptr, indices, values, num_cols, k, dim or 256)
+    if mode == "dense":
+        if indptr is None or values is None:
+            raise RuntimeError("backward_plan: mode 'dense' needs indptr= and values=")
+        return dense_plan(indptr, indices, values, num_cols)
     if mode == "bucket":
         return bucket_plan(indices, num_cols, k)
     if mode == "bsort":
@@ -726,6 +774,10 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     phase 2 reads a bucket's rows of a window as one run -- for large sparse graphs at small
     k, where a csc or bucket phase 2 pays a whole random line per 32-B row (bsort_plan()).
     mode "atomic": one global fp32 atomic per (edge, l); no preprocessing.
+    mode "dense" (k % 4 == 0, dim % 4 == 0; "auto" picks it at k >= dim / 2, dim <= 128,
+    maxk_dense_route): Y = A^T diag(1/row_div) G over dense G rows along the graph's transpose
+    with source rows (dense_plan), then the k selected columns of each row of Y; bitwise
+    repeatable.
     mode "hybrid" (k % 4 == 0; "auto" picks it on sparse graphs with locality): the pull
     over the dense tiles of the pull plan, on a second stream, beside csc over the other
     edges (hybrid_plan), for large graphs whose vertex order groups their communities."""
@@ -752,7 +804,24 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             raise RuntimeError("out must be [num_cols, k]")
     L = _lib()
     E = indices.numel()
+    asked = mode or os.environ.get("MAXK_BWD_MODE", "auto")
     mode = _bwd_mode(mode, k, E, num_cols, num_rows, D, (indptr, indices))
+    if mode == "dense":
+        aligned = (grad_output.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0
+                   and cbsr_idx.data_ptr() % 4 == 0)
+        if not aligned and asked == "auto":
+            mode, plan = "pull", None  # the dense kernels' vector loads need aligned rows
+    if mode == "dense":
+        col_ptr, t_src, t_w = (plan if plan is not None
+                               else dense_plan(indptr, indices, values, num_cols))
+        ws_bytes = L.maxk_sspmm_backward_dense_workspace_size(num_rows, num_cols, E, D, k, chunk)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        with _on(dev):
+            _capi.check(L.maxk_sspmm_backward_dense(
+                _ptr(col_ptr), _ptr(t_src), _ptr(t_w), _ptr(grad_output), _ptr(row_div),
+                _ptr(cbsr_idx), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws),
+                ws.numel(), _stream(dev)), "maxk_sspmm_backward_dense")
+        return out
     if mode == "hybrid":
         tl, te, bp, bt, ent, shift, S, off = (plan if plan is not None else
                                              hybrid_plan(indptr, indices, values, num_cols, k, D))

@@ -52,6 +52,11 @@ SIGNATURES = {
     "maxk_edge_selectors_blocks": (_i64, [_i64]),
     "maxk_transpose_plan_workspace_size": (_sz, [_i64, _i64]),
     "maxk_transpose_plan": (ctypes.c_int, [_p, _i64, _i64, _p, _p, _p, _sz, _p]),
+    "maxk_dense_route": (ctypes.c_int, [_i32, _i32]),
+    "maxk_dense_plan": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _p, _p]),
+    "maxk_sspmm_backward_dense_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
+    "maxk_sspmm_backward_dense": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
+                                                 _i32, _i32, _i32, _p, _sz, _p]),
     "maxk_sspmm_backward_bucket_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward_bucket": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p,
                                                   _i64, _i64, _i64, _i32, _i32, _i32, _p, _sz,

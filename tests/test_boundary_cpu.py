@@ -214,7 +214,23 @@ def test_backward_mode_resolution():
     with pytest.raises(RuntimeError):
         mk._bwd_mode("pull", 16, **reddit, dim=9)
     with pytest.raises(RuntimeError):
-        mk._bwd_mode("dense", 16, **reddit)
+        mk._bwd_mode("nope", 16, **reddit)
+    # k >= D / 2 at D <= 128 (r05): the dense route, both directions
+    assert mk._bwd_mode("dense", 16, **reddit) == "dense"
+    with pytest.raises(RuntimeError):
+        mk._bwd_mode("dense", 6, **reddit)
+    with pytest.raises(RuntimeError):
+        mk._bwd_mode("dense", 16, **reddit, dim=9)
+    assert mk._bwd_mode("auto", 32, **flickr, dim=64) == "dense"
+    assert mk._bwd_mode("auto", 64, **flickr, dim=64) == "dense"
+    assert mk._bwd_mode("auto", 28, **flickr, dim=64) == "pull"
+    assert mk._bwd_mode("auto", 64, **reddit, dim=128) == "dense"
+    assert mk._bwd_mode("auto", 128, **reddit, dim=256) != "dense"  # past MAXK_DENSE_DMAX
+    F = (flickr["num_rows"], flickr["num_cols"], flickr["num_e"])
+    assert L.maxk_backward_mode_auto(*F, 64, 32, -1.0) == 6   # MAXK_BWD_DENSE
+    assert L.maxk_backward_mode_auto(*F, -1, 32, -1.0) != 6   # dim unknown: no dense route
+    assert [L.maxk_dense_route(64, k) for k in (16, 30, 32, 64)] == [0, 0, 1, 1]
+    assert [L.maxk_dense_route(D, 64) for D in (100, 128, 132, 256)] == [1, 1, 0, 0]
 
 
 def test_bucket_shift_rule():

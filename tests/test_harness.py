@@ -23,7 +23,7 @@ def test_harness_builds_and_starts():
     assert os.access(BIN, os.X_OK), "make -C spgemm-prunning_amd builds bin/maxk_kernel_test"
     r = run("--help")
     assert r.returncode == 0 and "usage:" in r.stdout
-    r = run("--bwd", "dense", "g")
+    r = run("--bwd", "nope", "g")
     assert r.returncode == 1 and "--bwd" in r.stderr
 
 

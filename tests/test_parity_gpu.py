@@ -159,7 +159,7 @@ def test_edge_selector_stream_golden(mk, cuda, path, chunk):
     close(got, z["grad_cbsr_ref"])
 
 
-@pytest.mark.parametrize("mode", ["auto", "pull", "bucket", "bsort", "csc", "atomic"])
+@pytest.mark.parametrize("mode", ["auto", "pull", "bucket", "bsort", "csc", "atomic", "dense"])
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_backward_golden(mk, cuda, path, chunk, mode):
@@ -168,6 +168,8 @@ def test_backward_golden(mk, cuda, path, chunk, mode):
         pytest.skip(f"{mode} mode needs k % 4 == 0")
     if mode == "pull" and int(z["D"]) % 4:
         pytest.skip("pull mode needs D % 4 == 0")
+    if mode == "dense" and (int(z["D"]) % 4 or z["topk_idx"].shape[1] % 4):
+        pytest.skip("dense mode needs D % 4 == 0 and k % 4 == 0")
     gs = mk.sspmm_backward(T(z["row_ptr"], cuda), T(z["col_idx"], cuda), T(z["val"], cuda),
                            T(z["g"], cuda), T(z["topk_idx"], cuda), row_div=T(z["deg"], cuda),
                            chunk=chunk, mode=mode)
@@ -637,7 +639,8 @@ def run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div=None, chunk=0, mode=
 
 @pytest.mark.parametrize("k,D", [(1, 64), (2, 64), (3, 64), (8, 256), (16, 256), (24, 256),
                                  (32, 256), (48, 256), (64, 256), (96, 256), (128, 256),
-                                 (255, 256), (256, 256), (16, 100), (7, 9)])
+                                 (255, 256), (256, 256), (16, 100), (7, 9), (32, 64),
+                                 (64, 64), (52, 100), (64, 128), (128, 128)])
 def test_all_k_against_oracle(mk, cuda, k, D):
     rng = np.random.default_rng(k * 1000 + D)
     V = 600
@@ -654,6 +657,8 @@ def test_all_k_against_oracle(mk, cuda, k, D):
         modes += [(13, "bucket"), (0, "bsort")]
     if D % 4 == 0 and (k % 4 == 0 or k <= 64):
         modes.append((0, "pull"))
+    if D % 4 == 0 and k % 4 == 0:
+        modes += [(0, "dense"), (13, "dense"), (600, "dense")]
     for chunk, mode in modes:
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, div, chunk, mode)
         close(y, yo)
@@ -698,7 +703,7 @@ def test_empty_graph_and_empty_rows(mk, cuda):
     col = np.array([0, 5, 49], np.int32)
     val = np.array([1.0, 2.0, 3.0], np.float32)
     for chunk in (0, 1, 2, 7):
-        for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
+        for mode in ("pull", "bucket", "bsort", "csc", "atomic", "dense"):
             y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=chunk,
                                      mode=mode)
             close(y, yo)
@@ -720,7 +725,7 @@ def test_zero_rows(mk, cuda):
     y = mk.spgemm_forward(row_ptr, col, val, cv, ci, D)
     assert y.shape == (0, D)
     g = torch.zeros(0, D, device=cuda)
-    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic", "dense"):
         gs = torch.full((ncols, k), 7.0, device=cuda)
         mk.sspmm_backward(row_ptr, col, val, g, ci, out=gs, mode=mode)
         torch.cuda.synchronize()
@@ -739,7 +744,7 @@ def test_output_fully_overwritten(mk, cuda):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda), T(ci, cuda),
                           D, out=out, chunk=9)
     close(y, O.spgemm_fwd(row_ptr, col, val, cv, ci, D))
-    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic", "dense"):
         gout = torch.full((V, k), float("nan"), device=cuda)
         gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
                                T(ci, cuda), out=gout, mode=mode, chunk=7)
@@ -761,13 +766,15 @@ def test_duplicate_selectors_accumulate(mk, cuda):
     close(gs, go)
 
 
-@pytest.mark.parametrize("D,k", [(64, 16), (64, 64), (128, 32), (128, 8), (256, 16)])
+@pytest.mark.parametrize("D,k", [(64, 16), (64, 32), (64, 64), (100, 52), (128, 32), (128, 64),
+                                 (128, 8), (256, 16)])
 def test_forward_small_sparse_paths(mk, cuda, D, k):
-    """The small sparse graphs' forwards (r05): the pack-free kernel (D <= 128, fp64 LDS
-    copies over the caller's CBSR) and the streaming rows over packed records (D = 256), with
-    repeated selectors, selectors >= D, empty rows, hub rows split over items (chunk 40) and
-    rows past the streaming limit, against the oracle; the full-width oracle cut back to D is
-    the reference for selectors past D (they contribute nothing)."""
+    """The small sparse graphs' forwards (r05): the streaming rows over packed records and, at
+    k >= D / 2 (D <= 128), the dense route (CBSR scattered to dense rows, lane groups walking
+    rows into registers) in both directions, with repeated selectors, selectors >= D, empty
+    rows, hub rows split over items (chunk 40) and rows past the lane groups' limit, against
+    the oracle; the full-width oracle cut back to D is the reference for selectors past D (they
+    contribute nothing).  The dense backward is bitwise repeatable."""
     rng = np.random.default_rng(D * 100 + k)
     V = 3000
     row_ptr, col = rand_graph(rng, V, 9, hubs=((7, 900), (11, 70), (1500, 130)), empty=40)
@@ -791,6 +798,20 @@ def test_forward_small_sparse_paths(mk, cuda, D, k):
                           T(ci, cuda), D, row_div=T(div, cuda), chunk=chunk, validate=False,
                           out=acc, accumulate=True)
         close(acc, yo + 1.0)
+    assert mk._lib().maxk_dense_route(D, k) == int(k % 4 == 0 and D <= 128 and 2 * k >= D)
+    if k % 4 == 0 and D % 4 == 0:
+        g = rng.standard_normal((V, D), dtype=np.float32)
+        gpad = np.zeros((V, 256), np.float32)  # selectors >= D read 0
+        gpad[:, :D] = g
+        go = O.sspmm_bwd(row_ptr, col, val, gpad, ci, row_div=div)
+        args = (T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda), T(ci, cuda))
+        for chunk in (0, 40):
+            gs = mk.sspmm_backward(*args, row_div=T(div, cuda), chunk=chunk, mode="dense",
+                                   validate=False)
+            close(gs, go)
+            again = mk.sspmm_backward(*args, row_div=T(div, cuda), chunk=chunk, mode="dense",
+                                      validate=False)
+            assert torch.equal(gs, again)
 
 
 @pytest.mark.parametrize("k", [4, 12, 16, 32])
@@ -851,7 +872,7 @@ def test_selectors_past_D_read_zero(mk, cuda):
     y = mk.spgemm_forward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(cv, cuda),
                           T(ci, cuda), D, validate=False)
     close(y, yo)
-    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic", "dense"):
         gs = mk.sspmm_backward(T(row_ptr, cuda), T(col, cuda), T(val, cuda), T(g, cuda),
                                T(ci, cuda), mode=mode, validate=False)
         close(gs, go)
@@ -868,7 +889,7 @@ def test_rectangular_shard(mk, cuda):
     val = rng.random(col.size, dtype=np.float32)
     cv, ci = O.topk(rng.standard_normal((C, D), dtype=np.float32), k)
     g = rng.standard_normal((R, D), dtype=np.float32)
-    for mode in ("pull", "bucket", "bsort", "csc", "atomic"):
+    for mode in ("pull", "bucket", "bsort", "csc", "atomic", "dense"):
         y, yo, gs, go = run_both(mk, cuda, row_ptr, col, val, cv, ci, g, D, chunk=64, mode=mode)
         assert y.shape == (R, D) and gs.shape == (C, k)
         close(y, yo)
@@ -1045,7 +1066,7 @@ def test_hipgraph_capture(mk, cuda):
     close(out, z["y_ref"])
 
 
-@pytest.mark.parametrize("mode", ["pull", "bucket", "bsort", "csc", "hybrid", "atomic"])
+@pytest.mark.parametrize("mode", ["pull", "bucket", "bsort", "csc", "hybrid", "atomic", "dense"])
 def test_hipgraph_capture_default_validation(mk, cuda, monkeypatch, mode):
     """Default (validate-once) mode: the first call may be inside a capture; forward and the
     two-phase backward (with its plan built beforehand) both replay correctly."""
