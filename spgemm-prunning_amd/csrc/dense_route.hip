@@ -126,11 +126,19 @@ __device__ __forceinline__ void store_row4(float *dst, float4 a, bool has_div, f
     *p = a;
 }
 
-// SEL (the backward): a row complete in its item is stored as its k selected columns,
-// grad_cbsr[row, l] = row[sel[row, l]] (through a per-group LDS copy of the row); the owner of
-// a row split over items stores its partial to out (= Y) for dense_fixup_select_kernel.
+// Rows are owned by the item holding their token.  A row of at most `chunk` edges is walked
+// whole by its owner, past the item's end if it must (so an item walks at most 2 * chunk
+// tokens; the LDS stage holds that many edges); only a longer (hub) row is split at item ends:
+// its owner stores a partial, every later item it reaches stores a partial to its slab, and
+// slab_fixup_kernel (forward) / dense_fixup_select_kernel (backward) add the slabs in item
+// order.  (Finishing hub rows inside the walk -- the last item to reach one adding the slabs,
+// counted with a device-scope atomic -- measured 2.7x slower on Flickr: every device-scope
+// release / acquire writes back and invalidates the XCD's L2.)  SEL (the backward): a whole
+// row is stored as its k selected
+// columns, grad_cbsr[row, l] = row[sel[row, l]] (through a per-group LDS copy of the row); a hub
+// row's partials go to out (= Y) and the slabs for dense_fixup_select_kernel.
 template <int LR, int U, bool SEL>
-__global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
+__global__ __launch_bounds__(kBlock, U <= 4 ? 6 : 4) void dense_rows_kernel(
     const int32_t *__restrict__ ptr, const int32_t *__restrict__ idx, const float *__restrict__ w,
     const float *__restrict__ src_div, const float *__restrict__ X, int D,
     const float *__restrict__ dst_div, float *__restrict__ out, int add,
@@ -138,7 +146,7 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
     int chunk, int n_items, const uint8_t *__restrict__ sel, float *__restrict__ grad_cbsr,
     int k) {
     constexpr int NG = kWave / LR;  // lane groups (rows in flight) per wave
-    // per wave: ids and scales of the item's edges, then (SEL) one row copy per lane group
+    // per wave: ids and scales of 2 * chunk edges, then (SEL) one row copy per lane group
     extern __shared__ __attribute__((aligned(16))) int32_t s_stage[];
     const int wid = threadIdx.x / kWave;
     const int lane = lane_id();
@@ -153,9 +161,9 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
     const int64_t d1 = d0 + chunk < total ? d0 + chunk : total;
     int r = wave_first_row_token(ptr, num_rows, d0);
     const int64_t p_lo = d0 - r;  // the item's first edge (the tokens before d0 hold r rows)
-    int32_t *s_idx = s_stage + (size_t)wid * (2 * chunk + (SEL ? 4 * kWave : 0));
-    float *s_sc = reinterpret_cast<float *>(s_idx + chunk);
-    float *s_buf = s_sc + chunk;  // SEL: group g's row copy at g * 4 * LR
+    int32_t *s_idx = s_stage + (size_t)wid * (4 * chunk + (SEL ? 4 * kWave : 0));
+    float *s_sc = reinterpret_cast<float *>(s_idx + 2 * chunk);
+    float *s_buf = s_sc + 2 * chunk;  // SEL: group g's row copy at g * 4 * LR
     const uint32_t *__restrict__ sel32 = reinterpret_cast<const uint32_t *>(sel);
     const int kw = k >> 2;
     // SEL: the group's finished row -> its k selected columns (selw: this lane's selector word)
@@ -176,7 +184,8 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
         wave_lds_fence();  // the copy is reused by the group's next row
     };
     {
-        const int n_pos = (int)(num_e - p_lo < chunk ? num_e - p_lo : chunk);
+        const int64_t span = 2 * (int64_t)chunk;
+        const int n_pos = (int)(num_e - p_lo < span ? num_e - p_lo : span);
         for (int i = lane; i < n_pos; i += kWave) {
             const int c = idx[p_lo + i];
             const float wv = w[p_lo + i];
@@ -214,12 +223,14 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
         return a;
     };
 
-    // continuation of row r - 1 (its token precedes d0): this item's part goes to its slab
+    // continuation of hub row r - 1 (its token precedes d0): this item's part goes to its slab
     int cont = -1;
     if (r > 0) {
+        const int64_t rp = ptr[r - 1];
         int64_t se = (int64_t)ptr[r];
+        const bool hub = se - rp > chunk;
         if (d1 - r < se) se = d1 - r;
-        if (p_lo < se) {
+        if (hub && p_lo < se) {
             const float div = dst_div ? dst_div[r - 1] : 1.f;
             const float4 a = wave_row(p_lo, se);
             if (g == 0 && qok)
@@ -229,8 +240,9 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
     }
     if (lane == 0) slab_row[item] = cont;
 
+    const int lmax = chunk < kDenseGroupMax ? chunk : kDenseGroupMax;
     while (r < num_rows) {
-        // rows of at most kDenseGroupMax item edges by the lane groups
+        // whole rows of at most lmax edges by the lane groups
         {
             int wb = r;  // ptr window: rows [wb, wb + 64), one per lane
             int rpw = ptr[wb + lane <= num_rows ? wb + lane : num_rows];
@@ -239,7 +251,6 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
             int row = -1;       // this group's row and its edge range [t, te)
             int64_t t = 0, te = 0;
             float div = 1.f;
-            bool full = true;   // SEL: the row's edges all lie in this item
             auto assign = [&]() {
                 const uint64_t idle = __ballot(row < 0);
                 for (int gi = 0; gi < NG && !stop; ++gi) {
@@ -250,14 +261,12 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
                     }
                     const int64_t rb = __builtin_amdgcn_readlane(rpw, next - wb);
                     const int64_t re = __builtin_amdgcn_readlane(rpw, next + 1 - wb);
-                    const int64_t se = d1 - next - 1 < re ? d1 - next - 1 : re;
-                    if (next < num_rows && next + rb < d1 && se - rb <= kDenseGroupMax) {
+                    if (next < num_rows && next + rb < d1 && re - rb <= lmax) {
                         if (g == gi) {
                             row = next;
                             t = rb;
-                            te = se;
+                            te = re;
                             div = dst_div ? dst_div[next] : 1.f;  // arrives before the store
-                            if constexpr (SEL) full = se == re;
                         }
                         ++next;
                     } else {
@@ -285,11 +294,10 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
             while (__ballot(row >= 0)) {
                 const int crow = row;
                 const float cdiv = div;
-                const bool cfull = full;
                 const bool fin = crow >= 0 && t + U >= te;
                 // SEL: the finished row's selector word, in flight with the next step's gathers
                 uint32_t cselw = 0u;
-                if (SEL && fin && cfull && q < kw) cselw = sel32[(int64_t)crow * kw + q];
+                if (SEL && fin && q < kw) cselw = sel32[(int64_t)crow * kw + q];
                 if (fin) row = -1;
                 t += U;
                 assign();
@@ -303,7 +311,7 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
                     sc[u] = scn[u];
                 }
                 if (fin) {
-                    if (SEL && cfull)
+                    if constexpr (SEL)
                         select_store(crow, a, cselw);
                     else if (qok)
                         store_row4(out + (int64_t)crow * D + 4 * q, a, dst_div != nullptr, cdiv,
@@ -316,14 +324,15 @@ __global__ __launch_bounds__(kBlock, 6) void dense_rows_kernel(
         if (r >= num_rows) break;
         const int64_t rb = ptr[r];
         if (rb + r >= d1) break;
-        // a longer row by the whole wave (split at d1: the rest goes to the next items' slabs)
+        // a longer row by the whole wave: whole up to chunk edges, else a hub row split at d1
         const int64_t re = (int64_t)ptr[r + 1];
-        const int64_t se = d1 - r - 1 < re ? d1 - r - 1 : re;
+        const bool hub = re - rb > chunk;
+        const int64_t se = hub && d1 - r - 1 < re ? d1 - r - 1 : re;
         const float div = dst_div ? dst_div[r] : 1.f;
         const uint32_t selw = SEL && q < kw ? sel32[(int64_t)r * kw + q] : 0u;
         const float4 a = wave_row(rb, se);
         if (g == 0) {
-            if (SEL && se == re)
+            if (SEL && !hub)
                 select_store(r, a, selw);
             else if (qok)
                 store_row4(out + (int64_t)r * D + 4 * q, a, dst_div != nullptr, div, add != 0);
@@ -406,7 +415,7 @@ int dense_lanes(int D) {
 template <int LR>
 int rows_blocks_per_cu(bool sel) {
     int b = 0;
-    const size_t lds = (size_t)kWavesPerBlock * (256 * 8 + (sel ? 16 * kWave : 0));
+    const size_t lds = (size_t)kWavesPerBlock * (256 * 16 + (sel ? 16 * kWave : 0));
     const hipError_t e =
         sel ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                   &b, dense_rows_kernel<LR, MAXK_DENSE_U, true>, kBlock, lds)
@@ -483,7 +492,7 @@ int launch_dense_rows(const DenseLayout &L, hipStream_t s, const int32_t *ptr, c
                       float *grad_cbsr = nullptr, int k = 0) {
     const dim3 grid((unsigned)ceil_div(L.n_items, kWavesPerBlock));
     const bool select = sel != nullptr;
-    const size_t lds = (size_t)kWavesPerBlock * (L.chunk * 8 + (select ? 16 * kWave : 0));
+    const size_t lds = (size_t)kWavesPerBlock * (L.chunk * 16 + (select ? 16 * kWave : 0));
     constexpr int U = MAXK_DENSE_U;
     switch (dense_lanes(D)) {
 #define MAXK_CASE(LRV)                                                                          \
@@ -616,7 +625,8 @@ extern "C" int maxk_sspmm_backward_dense(const int32_t *col_ptr, const int32_t *
     int32_t *slab_row = reinterpret_cast<int32_t *>(ws + L.row_off);
     hipStream_t s = as_stream(stream);
     if (int rc = launch_dense_rows(L, s, col_ptr, t_src, t_w, row_div, grad_out, D, nullptr, Y, 0,
-                                   slab, slab_row, (int)num_cols, num_e, cbsr_idx, grad_cbsr, k))
+                                   slab, slab_row, (int)num_cols, num_e, cbsr_idx, grad_cbsr,
+                                   k))
         return rc;
     hipLaunchKernelGGL(dense_fixup_select_kernel, dim3((unsigned)ceil_div(L.n_items, kBlock / 16)),
                        dim3(kBlock), 0, s, slab, slab_row, Y, cbsr_idx, grad_cbsr, D, k,
