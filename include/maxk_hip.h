@@ -341,9 +341,11 @@ int maxk_pull_plan(const int32_t *row_ptr, const int32_t *col_idx, const float *
  *   maxk_transpose_plan (col_ptr, csc_eid), t_src[t] = the CSR row holding edge csc_eid[t] and
  *   t_w[t] = edge_val[csc_eid[t]] (int32 / float [num_e]).  Once per graph and weights.
  * maxk_sspmm_backward_dense: grad_cbsr[c, l] = (A^T diag(1/row_div) G)[c, cbsr_idx[c, l]] from
- *   the transpose plan: Y = A^T diag(1/row_div) G walked over dense G rows into the workspace,
- *   then the k selected columns of each row (selectors >= dim_origin read 0).  Bitwise
- *   repeatable.  16-B aligned grad_out and grad_cbsr, 4-B aligned cbsr_idx.
+ *   the transpose plan, walked destination by destination: at dim_k >= dim_origin / 2 over dense
+ *   G rows, each finished row stored as its k selected columns; below that (dim_k <= 64) one
+ *   selected column per lane, G[src, sel[c, l]] gathered per edge (selectors >= dim_origin read
+ *   0).  Any dim_k % 4 == 0 <= dim_origin; the route's rule (maxk_dense_route) is where "auto"
+ *   takes it.  Bitwise repeatable.  16-B aligned grad_out and grad_cbsr, 4-B aligned cbsr_idx.
  * ------------------------------------------------------------------------- */
 int maxk_dense_route(int32_t dim_origin, int32_t dim_k);
 int maxk_dense_plan(const int32_t *row_ptr, const float *edge_val, const int32_t *csc_eid,

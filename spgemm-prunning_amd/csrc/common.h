@@ -171,6 +171,9 @@ constexpr size_t kInfinityCacheBytes = 256ull << 20;  // MI355X MALL (MI355X_MIC
 #ifndef MAXK_DENSE_U  // dense_rows_kernel: edges per lane-group step (Flickr-sized D = 64,
 #define MAXK_DENSE_U 4  // k = 64: 0.094 ms at 8, 0.070 at 4)
 #endif
+#ifndef MAXK_DENSE_PICK  // the dense backward below k = D / 2: selected columns per lane
+#define MAXK_DENSE_PICK 1   // (pick_rows_kernel); 0 = dense rows and a selecting store
+#endif
 #ifndef MAXK_DENSE_WAVES  // dense_rows_kernel: resident waves per CU its item size assumes
 #define MAXK_DENSE_WAVES 24
 #endif

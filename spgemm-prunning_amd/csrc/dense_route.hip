@@ -341,6 +341,171 @@ __global__ __launch_bounds__(kBlock, U <= 4 ? 6 : 4) void dense_rows_kernel(
     }
 }
 
+// The backward at k < D / 2 (the destination-ordered walk without a dense Y): lane groups of
+// LR = pow2ceil(k) lanes, lane l of a group holding selector l of its destination row for the
+// whole row and gathering G[src, sel[c, l]] for each of the row's edges (one dword per lane;
+// the group's k columns of one G row share its few lines), summed in registers and stored as
+// grad_cbsr[c, l] directly.  Rows, items, staging and hub rows as in dense_rows_kernel; a hub
+// row's owner stores its partial to grad_cbsr and later items to their slabs (k floats), added
+// by slab_fixup_kernel<1>.  Selectors >= D read 0.
+template <int LR, int U>
+__global__ __launch_bounds__(kBlock, U <= 4 ? 6 : 4) void pick_rows_kernel(
+    const int32_t *__restrict__ ptr, const int32_t *__restrict__ idx, const float *__restrict__ w,
+    const float *__restrict__ src_div, const float *__restrict__ G, int D,
+    const uint8_t *__restrict__ sel, int k, float *__restrict__ grad_cbsr,
+    float *__restrict__ slab, int32_t *__restrict__ slab_row, int num_rows, int64_t num_e,
+    int chunk, int n_items) {
+    constexpr int NG = kWave / LR;
+    extern __shared__ __attribute__((aligned(16))) int32_t s_stage[];
+    const int wid = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int item = (int)blockIdx.x * kWavesPerBlock + wid;
+    if (item >= n_items) return;  // whole wave; no workgroup barrier below
+    const int g = lane / LR, q = lane % LR;
+    const bool qok = q < k;
+    const int64_t total = (int64_t)num_rows + num_e;
+    const int64_t d0 = (int64_t)item * chunk;
+    const int64_t d1 = d0 + chunk < total ? d0 + chunk : total;
+    int r = wave_first_row_token(ptr, num_rows, d0);
+    const int64_t p_lo = d0 - r;
+    int32_t *s_idx = s_stage + (size_t)wid * 4 * chunk;
+    float *s_sc = reinterpret_cast<float *>(s_idx + 2 * chunk);
+    {
+        const int64_t span = 2 * (int64_t)chunk;
+        const int n_pos = (int)(num_e - p_lo < span ? num_e - p_lo : span);
+        for (int i = lane; i < n_pos; i += kWave) {
+            const int c = idx[p_lo + i];
+            const float wv = w[p_lo + i];
+            s_idx[i] = c;
+            s_sc[i] = src_div ? wv / src_div[c] : wv;
+        }
+        wave_lds_fence();
+    }
+    // this lane's column of row c (D: reads 0)
+    auto col_of = [&](int c) -> int {
+        const int sv = qok ? (int)sel[(int64_t)c * k + q] : D;
+        return sv < D ? sv : D;
+    };
+    auto load = [&](int i, int col) -> float {
+        return col < D ? G[(size_t)(uint32_t)s_idx[i] * D + col] : 0.f;
+    };
+    auto wave_row = [&](int64_t sb, int64_t se, int col) -> float {
+        float a = 0.f;
+        for (int64_t base = sb; base < se; base += (int64_t)NG * U) {
+            float v[U], sc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t e = base + u * NG + g;
+                v[u] = 0.f;
+                sc[u] = 0.f;
+                if (e < se) {
+                    const int i = (int)(e - p_lo);
+                    sc[u] = s_sc[i];
+                    v[u] = load(i, col);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) a = __builtin_fmaf(sc[u], v[u], a);
+        }
+        for (int off = LR; off < kWave; off <<= 1) a += __shfl_xor(a, off);
+        return a;
+    };
+
+    int cont = -1;
+    if (r > 0) {
+        const int64_t rp = ptr[r - 1];
+        int64_t se = (int64_t)ptr[r];
+        const bool hub = se - rp > chunk;
+        if (d1 - r < se) se = d1 - r;
+        if (hub && p_lo < se) {
+            const float a = wave_row(p_lo, se, col_of(r - 1));
+            if (g == 0 && qok) slab[(int64_t)item * k + q] = a;
+            cont = r - 1;
+        }
+    }
+    if (lane == 0) slab_row[item] = cont;
+
+    const int lmax = chunk < kDenseGroupMax ? chunk : kDenseGroupMax;
+    while (r < num_rows) {
+        {
+            int wb = r;
+            int rpw = ptr[wb + lane <= num_rows ? wb + lane : num_rows];
+            int next = r;
+            bool stop = false;
+            int row = -1, col = D;
+            int64_t t = 0, te = 0;
+            auto assign = [&]() {
+                const uint64_t idle = __ballot(row < 0);
+                for (int gi = 0; gi < NG && !stop; ++gi) {
+                    if (!((idle >> (gi * LR)) & 1ull)) continue;
+                    if (next + 1 >= wb + kWave) {
+                        wb = next;
+                        rpw = ptr[wb + lane <= num_rows ? wb + lane : num_rows];
+                    }
+                    const int64_t rb = __builtin_amdgcn_readlane(rpw, next - wb);
+                    const int64_t re = __builtin_amdgcn_readlane(rpw, next + 1 - wb);
+                    if (next < num_rows && next + rb < d1 && re - rb <= lmax) {
+                        if (g == gi) {
+                            row = next;
+                            t = rb;
+                            te = re;
+                            col = col_of(next);
+                        }
+                        ++next;
+                    } else {
+                        stop = true;
+                    }
+                }
+            };
+            auto gather = [&](float (&v)[U], float (&sc)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    v[u] = 0.f;
+                    sc[u] = 0.f;
+                    if (row >= 0 && t + u < te) {
+                        const int i = (int)(t + u - p_lo);
+                        sc[u] = s_sc[i];
+                        v[u] = load(i, col);
+                    }
+                }
+            };
+            assign();
+            float v[U], sc[U];
+            gather(v, sc);
+            float a = 0.f;
+            while (__ballot(row >= 0)) {
+                const int crow = row;
+                const bool fin = crow >= 0 && t + U >= te;
+                if (fin) row = -1;
+                t += U;
+                assign();
+                float vn[U], scn[U];
+                gather(vn, scn);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    a = __builtin_fmaf(sc[u], v[u], a);
+                    v[u] = vn[u];
+                    sc[u] = scn[u];
+                }
+                if (fin) {
+                    if (qok) grad_cbsr[(int64_t)crow * k + q] = a;
+                    a = 0.f;
+                }
+            }
+            r = next;
+        }
+        if (r >= num_rows) break;
+        const int64_t rb = ptr[r];
+        if (rb + r >= d1) break;
+        const int64_t re = (int64_t)ptr[r + 1];
+        const bool hub = re - rb > chunk;
+        const int64_t se = hub && d1 - r - 1 < re ? d1 - r - 1 : re;
+        const float a = wave_row(rb, se, col_of(r));
+        if (g == 0 && qok) grad_cbsr[(int64_t)r * k + q] = a;  // a hub row's owner: its partial
+        ++r;
+    }
+}
+
 // The rows split over items (the backward): per run of items continuing one row, the owner's
 // partial Y[row] plus the slabs in item order (dense_rows_kernel's slab rule, as
 // slab_fixup_kernel), then the row's k selected columns into grad_cbsr.  16 lanes per item.
@@ -412,15 +577,18 @@ int dense_lanes(int D) {
 // that launches, times the CUs; MAXK_DENSE_WAVES per CU x 256 CUs when no device answers).
 // Cached per (lane group, SEL): the item size, and so the workspace size, stays the same for
 // the whole process.
+// kind: 0 dense_rows_kernel, 1 its selecting form, 2 pick_rows_kernel
 template <int LR>
-int rows_blocks_per_cu(bool sel) {
+int rows_blocks_per_cu(int kind) {
     int b = 0;
-    const size_t lds = (size_t)kWavesPerBlock * (256 * 16 + (sel ? 16 * kWave : 0));
+    const size_t lds = (size_t)kWavesPerBlock * (256 * 16 + (kind == 1 ? 16 * kWave : 0));
     const hipError_t e =
-        sel ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                  &b, dense_rows_kernel<LR, MAXK_DENSE_U, true>, kBlock, lds)
-            : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                  &b, dense_rows_kernel<LR, MAXK_DENSE_U, false>, kBlock, lds);
+        kind == 2   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                          &b, pick_rows_kernel<LR, MAXK_DENSE_U>, kBlock, lds)
+        : kind == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                          &b, dense_rows_kernel<LR, MAXK_DENSE_U, true>, kBlock, lds)
+                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                          &b, dense_rows_kernel<LR, MAXK_DENSE_U, false>, kBlock, lds);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return 0;
@@ -428,22 +596,21 @@ int rows_blocks_per_cu(bool sel) {
     return b;
 }
 
-int64_t dense_slots(int D, bool sel) {
-    static int64_t cache[8][2] = {};
-    const int lr = dense_lanes(D);
+int64_t dense_slots(int lr, int kind) {
+    static int64_t cache[8][3] = {};
     int li = 0;
     while ((1 << li) < lr) ++li;
-    int64_t &c = cache[li][sel ? 1 : 0];
+    int64_t &c = cache[li][kind];
     if (c == 0) {
         int bpc = 0;
         switch (lr) {
-            case 1: bpc = rows_blocks_per_cu<1>(sel); break;
-            case 2: bpc = rows_blocks_per_cu<2>(sel); break;
-            case 4: bpc = rows_blocks_per_cu<4>(sel); break;
-            case 8: bpc = rows_blocks_per_cu<8>(sel); break;
-            case 16: bpc = rows_blocks_per_cu<16>(sel); break;
-            case 32: bpc = rows_blocks_per_cu<32>(sel); break;
-            default: bpc = rows_blocks_per_cu<64>(sel); break;
+            case 1: bpc = rows_blocks_per_cu<1>(kind); break;
+            case 2: bpc = rows_blocks_per_cu<2>(kind); break;
+            case 4: bpc = rows_blocks_per_cu<4>(kind); break;
+            case 8: bpc = rows_blocks_per_cu<8>(kind); break;
+            case 16: bpc = rows_blocks_per_cu<16>(kind); break;
+            case 32: bpc = rows_blocks_per_cu<32>(kind); break;
+            default: bpc = rows_blocks_per_cu<64>(kind); break;
         }
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -472,14 +639,20 @@ struct DenseLayout {
 
 // x_rows: rows of the dense table the route writes (forward: num_cols source rows of X;
 // backward: num_cols destination rows of Y)
-DenseLayout dense_layout(int64_t rows, int64_t x_rows, int64_t num_e, int D, int chunk, bool sel) {
+// the backward picks selected columns (pick_rows_kernel) below k = D / 2 (MAXK_DENSE_PICK)
+bool dense_pick(int D, int k) { return MAXK_DENSE_PICK && 2 * k < D && k <= kWave; }
+
+// kind as rows_blocks_per_cu; width: floats per slab row (D, or k for the pick)
+DenseLayout dense_layout(int64_t rows, int64_t x_rows, int64_t num_e, int D, int chunk, int kind,
+                         int width) {
     DenseLayout L{};
-    L.chunk = dense_chunk(rows + num_e, chunk, dense_slots(D, sel));
+    L.chunk = dense_chunk(rows + num_e, chunk,
+                          dense_slots(kind == 2 ? lanes_per_edge(width) : dense_lanes(D), kind));
     const int64_t n = ceil_div(rows + num_e, L.chunk);
     L.n_items = (int)(n > 0 ? n : 1);
     L.x_off = 0;
     L.slab_off = al256((size_t)x_rows * D * sizeof(float));
-    L.row_off = L.slab_off + al256((size_t)L.n_items * D * sizeof(float));
+    L.row_off = L.slab_off + al256((size_t)L.n_items * width * sizeof(float));
     L.total = L.row_off + al256((size_t)L.n_items * sizeof(int32_t));
     return L;
 }
@@ -530,7 +703,7 @@ bool dense_route(int D, int k) {
 
 size_t dense_forward_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e, int D,
                                     int chunk) {
-    return dense_layout(num_rows, num_cols, num_e, D, chunk, false).total;
+    return dense_layout(num_rows, num_cols, num_e, D, chunk, 0, D).total;
 }
 
 int dense_forward(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
@@ -538,7 +711,7 @@ int dense_forward(const int32_t *row_ptr, const int32_t *col_idx, const float *e
                   float *out, int64_t num_rows, int64_t num_cols, int64_t num_e, int D, int k,
                   int chunk, void *workspace, size_t workspace_bytes, hipStream_t s,
                   int accumulate) {
-    const DenseLayout L = dense_layout(num_rows, num_cols, num_e, D, chunk, false);
+    const DenseLayout L = dense_layout(num_rows, num_cols, num_e, D, chunk, 0, D);
     MAXK_REQUIRE(workspace && workspace_bytes >= L.total,
                  "workspace too small: need %zu bytes, got %zu", L.total, workspace_bytes);
     char *ws = reinterpret_cast<char *>(workspace);
@@ -588,9 +761,10 @@ extern "C" size_t maxk_sspmm_backward_dense_workspace_size(int64_t num_rows, int
                                                            int64_t num_e, int32_t dim_origin,
                                                            int32_t dim_k, int32_t chunk_edges) {
     (void)num_rows;
-    (void)dim_k;
-    if (num_cols < 0 || num_e < 0 || dim_origin <= 0) return 0;
-    return dense_layout(num_cols, num_cols, num_e, dim_origin, chunk_edges, true).total;
+    if (num_cols < 0 || num_e < 0 || dim_origin <= 0 || dim_k <= 0) return 0;
+    const int D = dim_origin, k = dim_k;
+    if (dense_pick(D, k)) return dense_layout(num_cols, 0, num_e, D, chunk_edges, 2, k).total;
+    return dense_layout(num_cols, num_cols, num_e, D, chunk_edges, 1, D).total;
 }
 
 extern "C" int maxk_sspmm_backward_dense(const int32_t *col_ptr, const int32_t *t_src,
@@ -616,14 +790,46 @@ extern "C" int maxk_sspmm_backward_dense(const int32_t *col_ptr, const int32_t *
     MAXK_REQUIRE(((uintptr_t)cbsr_idx & 3) == 0 && ((uintptr_t)grad_cbsr & 15) == 0 &&
                      ((uintptr_t)grad_out & 15) == 0,
                  "dense backward needs 4-B aligned selectors and 16-B aligned G / grad_cbsr");
-    const DenseLayout L = dense_layout(num_cols, num_cols, num_e, D, chunk_edges, true);
+    hipStream_t s = as_stream(stream);
+    if (dense_pick(D, k)) {
+        const DenseLayout L = dense_layout(num_cols, 0, num_e, D, chunk_edges, 2, k);
+        MAXK_REQUIRE(workspace && workspace_bytes >= L.total,
+                     "workspace too small: need %zu bytes, got %zu", L.total, workspace_bytes);
+        char *ws = reinterpret_cast<char *>(workspace);
+        float *slab = reinterpret_cast<float *>(ws + L.slab_off);
+        int32_t *slab_row = reinterpret_cast<int32_t *>(ws + L.row_off);
+        const dim3 grid((unsigned)ceil_div(L.n_items, kWavesPerBlock));
+        const size_t lds = (size_t)kWavesPerBlock * L.chunk * 16;
+        constexpr int U = MAXK_DENSE_U;
+        switch (lanes_per_edge(k)) {
+#define MAXK_CASE(LRV)                                                                         \
+    case LRV:                                                                                  \
+        hipLaunchKernelGGL((pick_rows_kernel<LRV, U>), grid, dim3(kBlock), lds, s, col_ptr,    \
+                           t_src, t_w, row_div, grad_out, D, cbsr_idx, k, grad_cbsr, slab,     \
+                           slab_row, (int)num_cols, num_e, L.chunk, L.n_items);               \
+        break;
+            MAXK_CASE(1)
+            MAXK_CASE(2)
+            MAXK_CASE(4)
+            MAXK_CASE(8)
+            MAXK_CASE(16)
+            MAXK_CASE(32)
+            MAXK_CASE(64)
+#undef MAXK_CASE
+            default:
+                set_error("unsupported lane group for k = %d", k);
+                return MAXK_ERR_INVALID;
+        }
+        MAXK_LAUNCHED("pick_rows_kernel");
+        return launch_slab_fixup<1>(slab, slab_row, grad_cbsr, k, L.n_items, s);
+    }
+    const DenseLayout L = dense_layout(num_cols, num_cols, num_e, D, chunk_edges, 1, D);
     MAXK_REQUIRE(workspace && workspace_bytes >= L.total,
                  "workspace too small: need %zu bytes, got %zu", L.total, workspace_bytes);
     char *ws = reinterpret_cast<char *>(workspace);
     float *Y = reinterpret_cast<float *>(ws + L.x_off);
     float *slab = reinterpret_cast<float *>(ws + L.slab_off);
     int32_t *slab_row = reinterpret_cast<int32_t *>(ws + L.row_off);
-    hipStream_t s = as_stream(stream);
     if (int rc = launch_dense_rows(L, s, col_ptr, t_src, t_w, row_div, grad_out, D, nullptr, Y, 0,
                                    slab, slab_row, (int)num_cols, num_e, cbsr_idx, grad_cbsr,
                                    k))
