@@ -128,14 +128,15 @@ def test_sharded_nccl_one_gpu_per_rank(graph, single, world):
 
 
 @pytest.mark.parametrize("stream", ["0", "1"])
-@pytest.mark.parametrize("bwd", ["bsort", "csc"])
+@pytest.mark.parametrize("bwd", ["bsort", "csc", "dense"])
 def test_sharded_forced_backward_modes(graph, single, bwd, stream, monkeypatch):
     """World 2 with every shard's backward forced to the two-phase forms a large sparse graph
     resolves to (window-sorted at k <= 8, csc above): the shards' column spaces are the padded
     gathered ones (gather mode) or the compact halos (halo mode), their plans built per shard
     and pipeline part; with MAXK_EDGE_SEL=1 every pipeline part's forward also writes its
     edge-selector stream (the later parts through maxk_spgemm_forward_accumulate_sel) and its
-    backward reads it."""
+    backward reads it.  "dense" (selected columns gathered along each shard's transpose, r05)
+    reads no stream."""
     monkeypatch.setenv("MAXK_BWD_MODE", bwd)
     monkeypatch.setenv("MAXK_EDGE_SEL", stream)
     _run_world(graph, single, 2, "gloo")

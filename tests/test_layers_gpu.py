@@ -72,7 +72,7 @@ def test_maxk_nonlinearity_grad(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dim,k", [(64, 8), (256, 32)])
+@pytest.mark.parametrize("dim,k", [(64, 8), (256, 32), (64, 32), (64, 64)])  # k >= dim / 2: dense route
 def test_sage_conv(cuda, dim, k):
     import maxk_layers
 
