@@ -52,8 +52,9 @@ TAG_RATE_PER_S = 256 * 2.4e9
 
 # kernels making up each op of one step (rocprofv3 names, maxk:: namespace)
 OP_KERNELS = {
+    # the record route, or (k >= D / 2, D <= 128) the dense route (dense_route.hip)
     "spgemm_forward": ["spgemm_fwd_kernel", "slab_fixup_kernel<0>", "cbsr_pack4_kernel",
-                       "cbsr_pack_kernel"],
+                       "cbsr_pack_kernel", "cbsr_dense_kernel", "dense_rows_kernel"],
     "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>"],
     # k % 4 == 0: slot-ordered selectors, quantile-slot tiles; else pull_tile_kernel; plus
     # gprime_kernel when a row_div is given (the bench passes none)
@@ -62,6 +63,9 @@ OP_KERNELS = {
     "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_bsort": ["bsort_push_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
+    # dense rows with the selecting store (k >= D / 2), or selected columns per lane
+    "sspmm_backward_dense": ["dense_select_rows_kernel", "dense_fixup_select_kernel",
+                             "pick_rows_kernel", "slab_fixup_kernel<1>"],
     # csc over the sparse tiles' edges, then the pull over the dense ones, accumulating
     "sspmm_backward_hybrid": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>",
                               "pull_sel4_kernel", "pull_sel_kernel", "pull_q_kernel",

@@ -138,7 +138,7 @@ __device__ __forceinline__ void store_row4(float *dst, float4 a, bool has_div, f
 // columns, grad_cbsr[row, l] = row[sel[row, l]] (through a per-group LDS copy of the row); a hub
 // row's partials go to out (= Y) and the slabs for dense_fixup_select_kernel.
 template <int LR, int U, bool SEL>
-__global__ __launch_bounds__(kBlock, U <= 4 ? 6 : 4) void dense_rows_kernel(
+__device__ __forceinline__ void dense_rows_body(
     const int32_t *__restrict__ ptr, const int32_t *__restrict__ idx, const float *__restrict__ w,
     const float *__restrict__ src_div, const float *__restrict__ X, int D,
     const float *__restrict__ dst_div, float *__restrict__ out, int add,
@@ -339,6 +339,27 @@ __global__ __launch_bounds__(kBlock, U <= 4 ? 6 : 4) void dense_rows_kernel(
         }
         ++r;
     }
+}
+
+// The forward walk and the backward's selecting walk as two kernels (two names in profiles)
+template <int LR, int U>
+__global__ __launch_bounds__(kBlock, U <= 4 ? 6 : 4) void dense_rows_kernel(
+    const int32_t *__restrict__ ptr, const int32_t *__restrict__ idx, const float *__restrict__ w,
+    const float *__restrict__ X, int D, const float *__restrict__ dst_div, float *__restrict__ out,
+    int add, float *__restrict__ slab, int32_t *__restrict__ slab_row, int num_rows,
+    int64_t num_e, int chunk, int n_items) {
+    dense_rows_body<LR, U, false>(ptr, idx, w, nullptr, X, D, dst_div, out, add, slab, slab_row,
+                                  num_rows, num_e, chunk, n_items, nullptr, nullptr, 0);
+}
+template <int LR, int U>
+__global__ __launch_bounds__(kBlock, U <= 4 ? 6 : 4) void dense_select_rows_kernel(
+    const int32_t *__restrict__ ptr, const int32_t *__restrict__ idx, const float *__restrict__ w,
+    const float *__restrict__ src_div, const float *__restrict__ X, int D, float *__restrict__ Y,
+    float *__restrict__ slab, int32_t *__restrict__ slab_row, int num_rows, int64_t num_e,
+    int chunk, int n_items, const uint8_t *__restrict__ sel, float *__restrict__ grad_cbsr,
+    int k) {
+    dense_rows_body<LR, U, true>(ptr, idx, w, src_div, X, D, nullptr, Y, 0, slab, slab_row,
+                                 num_rows, num_e, chunk, n_items, sel, grad_cbsr, k);
 }
 
 // The backward at k < D / 2 (the destination-ordered walk without a dense Y): lane groups of
@@ -586,9 +607,9 @@ int rows_blocks_per_cu(int kind) {
         kind == 2   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                           &b, pick_rows_kernel<LR, MAXK_DENSE_U>, kBlock, lds)
         : kind == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                          &b, dense_rows_kernel<LR, MAXK_DENSE_U, true>, kBlock, lds)
+                          &b, dense_select_rows_kernel<LR, MAXK_DENSE_U>, kBlock, lds)
                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                          &b, dense_rows_kernel<LR, MAXK_DENSE_U, false>, kBlock, lds);
+                          &b, dense_rows_kernel<LR, MAXK_DENSE_U>, kBlock, lds);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return 0;
@@ -671,13 +692,13 @@ int launch_dense_rows(const DenseLayout &L, hipStream_t s, const int32_t *ptr, c
 #define MAXK_CASE(LRV)                                                                          \
     case LRV:                                                                                   \
         if (select)                                                                             \
-            hipLaunchKernelGGL((dense_rows_kernel<LRV, U, true>), grid, dim3(kBlock), lds, s,   \
-                               ptr, idx, w, src_div, X, D, dst_div, out, add, slab, slab_row,   \
-                               rows, num_e, L.chunk, L.n_items, sel, grad_cbsr, k);             \
+            hipLaunchKernelGGL((dense_select_rows_kernel<LRV, U>), grid, dim3(kBlock), lds, s,  \
+                               ptr, idx, w, src_div, X, D, out, slab, slab_row, rows, num_e,    \
+                               L.chunk, L.n_items, sel, grad_cbsr, k);                          \
         else                                                                                    \
-            hipLaunchKernelGGL((dense_rows_kernel<LRV, U, false>), grid, dim3(kBlock), lds, s,  \
-                               ptr, idx, w, src_div, X, D, dst_div, out, add, slab, slab_row,   \
-                               rows, num_e, L.chunk, L.n_items, nullptr, nullptr, 0);           \
+            hipLaunchKernelGGL((dense_rows_kernel<LRV, U>), grid, dim3(kBlock), lds, s, ptr,    \
+                               idx, w, X, D, dst_div, out, add, slab, slab_row, rows, num_e,    \
+                               L.chunk, L.n_items);                                             \
         break;
         MAXK_CASE(1)
         MAXK_CASE(2)
@@ -691,7 +712,7 @@ int launch_dense_rows(const DenseLayout &L, hipStream_t s, const int32_t *ptr, c
             set_error("unsupported dense lane group for D = %d", D);
             return MAXK_ERR_INVALID;
     }
-    MAXK_LAUNCHED("dense_rows_kernel");
+    MAXK_LAUNCHED(select ? "dense_select_rows_kernel" : "dense_rows_kernel");
     return MAXK_OK;
 }
 
