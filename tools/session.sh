@@ -12,7 +12,7 @@
 #   stats     rocprofv3 --kernel-trace --stats of a short default bench
 #   pmc       FETCH_SIZE and WRITE_SIZE of the same short bench, one rocprofv3 --pmc pass each
 #   presets   every preset with its denominators (rocSPARSE every algorithm; CPU baselines
-#             with PRESET_CPU=1)
+#             with PRESET_CPU=1); presets_small: the Flickr-shaped ones alone
 #   pmccfg    PMC passes of the non-default configurations in $CFGS
 #             ("name:--bench --args name2:..."), keyed by each run's traffic_key
 #   pmcset    counter sets $SETS ("C1 C2;C3 C4", one pass per set) over the configurations in
@@ -95,8 +95,14 @@ step_presets() {
   for k in 8 16 32 64; do preset products_k$k --graph products --k $k; done
   preset products_k4 --graph products --k 4 --no-rocsparse
   preset proteins --graph proteins
-  preset flickr --graph flickr
+  step_presets_small
   preset products_comm_ordered --graph products_comm --reorder
+}
+# the Flickr-shaped graph (configs[0], D = 64) at every k: k >= 32 takes the dense route
+step_presets_small() {
+  mkdir -p $O/presets
+  preset flickr --graph flickr
+  for k in 8 32 64; do preset flickr_k$k --graph flickr --k $k; done
 }
 cfg_loop() {  # cfg_loop <function>: $CFGS "name:--args ..." -> function name "args"
   local fn=$1 name="" args="" w
