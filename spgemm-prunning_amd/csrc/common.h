@@ -177,6 +177,12 @@ constexpr size_t kInfinityCacheBytes = 256ull << 20;  // MI355X MALL (MI355X_MIC
 #ifndef MAXK_DENSE_WAVES  // dense_rows_kernel: resident waves per CU its item size assumes
 #define MAXK_DENSE_WAVES 24
 #endif
+#ifndef MAXK_CSC_GROUP_DEG  // csc phase 2: lane groups per destination (csc_groups) below this
+#define MAXK_CSC_GROUP_DEG 16  // average in-degree (slots per destination); 0 = off
+#endif
+#ifndef MAXK_CSC_GROUP_U  // csc_groups: slots per lane-group step
+#define MAXK_CSC_GROUP_U 4
+#endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
 #endif

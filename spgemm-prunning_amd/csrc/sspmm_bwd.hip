@@ -391,13 +391,95 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T, EidAt e
     }
 }
 
+// Grouped destinations (low average in-degree, e.g. the halo columns of an N = 8 shard, ~6
+// slots each, where segment_sum spends one wave step and a 3-stage butterfly per destination).
+// Each lane group of LR = k/4 lanes walks one destination's slots U at a time into its own
+// float4 (in slot order: bitwise the same run to run), stores the row the step it ends and takes
+// the item's next destination, so 64/LR destinations are in flight per wave; the next step's
+// gathers are issued before this step's sums.  Destinations are taken in order while owned by
+// the item (token < d1) and holding at most lmax of its slots; returns the first one not taken
+// (the caller sums a longer one with the whole wave).  k % 4 == 0.
+template <int U, typename EidAt>
+__device__ __forceinline__ int csc_groups(const float *__restrict__ T, EidAt eid_at,
+                                          const int32_t *__restrict__ col_ptr, int c,
+                                          int num_cols, int64_t d1, int k, int lmax,
+                                          float *__restrict__ grad_cbsr, int lane) {
+    const int LR = k / 4, NG = kWave / LR;
+    const int g = lane / LR, q = lane % LR;
+    const float4 *__restrict__ T4 = reinterpret_cast<const float4 *>(T);
+    int wb = c;  // col_ptr window: destinations [wb, wb + 64), one per lane
+    int cpw = col_ptr[wb + lane <= num_cols ? wb + lane : num_cols];
+    int next = c;       // the next destination to hand out (wave-uniform)
+    bool stop = false;  // it is not the item's or is too long (wave-uniform)
+    int dst = -1;       // this group's destination and its slot range [t, te)
+    int64_t t = 0, te = 0;
+    auto assign = [&]() {
+        const uint64_t idle = __ballot(dst < 0);
+        for (int gi = 0; gi < NG && !stop; ++gi) {
+            if (!((idle >> (gi * LR)) & 1ull)) continue;
+            if (next + 1 >= wb + kWave) {  // slide the window (wave-uniform)
+                wb = next;
+                cpw = col_ptr[wb + lane <= num_cols ? wb + lane : num_cols];
+            }
+            const int64_t cb = __builtin_amdgcn_readlane(cpw, next - wb);
+            int64_t se = __builtin_amdgcn_readlane(cpw, next + 1 - wb);
+            if (d1 - next - 1 < se) se = d1 - next - 1;
+            if (next < num_cols && next + cb < d1 && se - cb <= lmax) {
+                if (g == gi) {
+                    dst = next;
+                    t = cb;
+                    te = se;
+                }
+                ++next;
+            } else {
+                stop = true;
+            }
+        }
+    };
+    auto gather = [&](float4 (&v)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (dst >= 0 && t + u < te) v[u] = T4[(size_t)(uint32_t)eid_at(t + u) * LR + q];
+        }
+    };
+    assign();
+    float4 v[U];
+    gather(v);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    while (__ballot(dst >= 0)) {
+        const int cdst = dst;
+        const bool fin = cdst >= 0 && t + U >= te;
+        if (fin) dst = -1;
+        t += U;
+        assign();
+        float4 vn[U];
+        gather(vn);  // the next step's rows in flight while this step's are summed
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a.x += v[u].x;
+            a.y += v[u].y;
+            a.z += v[u].z;
+            a.w += v[u].w;
+            v[u] = vn[u];
+        }
+        if (fin) {
+            reinterpret_cast<float4 *>(grad_cbsr + (int64_t)cdst * k)[q] = a;
+            a = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    return next;
+}
+
 // STAGED (chunk <= kCscStage): the item's CSC slots are one contiguous range of csc_eid,
 // starting at d0 - c (the tokens before d0 hold c destination tokens), so the wave copies
 // up to `chunk` of them into LDS with coalesced loads before its first segment: every T-row
 // gather then waits for one load instead of two dependent ones (a destination of ogbn-products
 // averages 50 slots, two U-steps, so each step used to wait for its eid loads first).
 constexpr int kCscStage = 2048;
-template <bool VEC, int KG, int U, bool STAGED>
+// GROUP (VEC, STAGED): destinations of at most kCscGroupMax slots go through csc_groups.
+constexpr int kCscGroupMax = 64;
+template <bool VEC, int KG, int U, bool STAGED, bool GROUP = false>
 __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restrict__ col_ptr,
                                                          const int32_t *__restrict__ eid,
                                                          const float *__restrict__ T,
@@ -443,6 +525,11 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
     }
     if (lane == 0) slab_row[item] = cont;
     for (; c < num_cols; ++c) {
+        if constexpr (GROUP) {
+            c = csc_groups<U>(T, eid_at, col_ptr, c, num_cols, d1, k, kCscGroupMax, grad_cbsr,
+                              lane);
+            if (c >= num_cols) break;
+        }
         const int64_t cb = col_ptr[c];
         if (cb + c >= d1) break;
         int64_t se = (int64_t)col_ptr[c + 1];
@@ -1560,7 +1647,13 @@ int csc_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_v
     const int nc = (int)num_cols;
     const bool staged = MAXK_CSC_STAGE && L.chunk <= kCscStage;
     const size_t lds = (size_t)kWavesPerBlock * L.chunk * sizeof(int32_t);
-    if (vec_sum(k)) {
+    if (staged && vec_sum(k) && k >= 16 && k <= 64 &&
+        num_e < (int64_t)MAXK_CSC_GROUP_DEG * num_cols) {
+        // few slots per destination: lane groups per destination (csc_groups)
+        hipLaunchKernelGGL((csc_sum_kernel<true, 64, MAXK_CSC_GROUP_U, true, true>), grid,
+                           dim3(kBlock), lds, s, col_ptr, csc_eid, T, grad_cbsr, slab, slab_row,
+                           nc, num_e, k, L.chunk, L.n_items);
+    } else if (vec_sum(k)) {
         const int rows_per_step = kWave / (k / 4);
         const int u = MAXK_SUM_U > 0 ? MAXK_SUM_U
                                      : pick_depth(num_e, num_cols, rows_per_step, 2, 8);
