@@ -1,12 +1,11 @@
-# r05 session: phase-1 item size at N = 8 (items floor at 256 tokens there): base (16 items per
-# slot), q4 / q2 (4 / 2 per slot: ~480 / ~960 tokens); shard probe at N = 1 and 8
+# r05 session: record stride in 32-B multiples once 128-B records outgrow the Infinity Cache
+# (products k = 16: 96-B records, 235 MB instead of 313 MB) -- parity on the variant, then the
+# bench forward A/B on products k = 16 / 8 / 12
 set -eo pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r05/s18
+O=gpurun_out/r05/s19
 mkdir -p $O
-for rep in 1 2; do
-for v in base q4 q2; do
-  lib=spgemm-prunning_amd/lib/variants/$v/libmaxk_hip.so; [ $v = base ] && lib=spgemm-prunning_amd/lib/libmaxk_hip.so
-  MAXK_HIP_LIB=$lib timeout -k 10 300 python tools/shard_probe.py --graph products --k 32 --worlds 1 8 > $O/shard_${v}_$rep.txt 2>&1
-done
-done
+MAXK_HIP_LIB=spgemm-prunning_amd/lib/variants/rs/libmaxk_hip.so timeout -k 10 600 python -u -m pytest tests/test_parity_gpu.py tests/test_fuzz_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_rs.log 2>&1 || { tail -40 $O/pytest_rs.log; exit 1; }
+tail -1 $O/pytest_rs.log
+R=2 timeout -k 10 900 bash tools/ab_bench.sh "base rs" "--graph products --k 16" "--graph products --k 12" > $O/ab.txt 2>&1
+cat $O/ab.txt
