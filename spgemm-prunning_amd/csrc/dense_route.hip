@@ -21,6 +21,8 @@
 // item's slab; slab_fixup_kernel adds the slabs in item order), are walked by the whole wave,
 // edges interleaved over the groups and the groups combined by xor butterflies.  Sums run in
 // edge order per lane: bitwise the same run to run.
+#include <atomic>
+
 #include "common.h"
 
 namespace maxk {
@@ -618,10 +620,10 @@ int rows_blocks_per_cu(int kind) {
 }
 
 int64_t dense_slots(int lr, int kind) {
-    static int64_t cache[8][3] = {};
+    static std::atomic<int64_t> cache[8][3] = {};  // every thread computes the same value
     int li = 0;
     while ((1 << li) < lr) ++li;
-    int64_t &c = cache[li][kind];
+    int64_t c = cache[li][kind].load(std::memory_order_relaxed);
     if (c == 0) {
         int bpc = 0;
         switch (lr) {
@@ -639,6 +641,7 @@ int64_t dense_slots(int lr, int kind) {
             cus = 0;
         (void)hipGetLastError();
         c = bpc > 0 && cus > 0 ? (int64_t)bpc * kWavesPerBlock * cus : 256LL * MAXK_DENSE_WAVES;
+        cache[li][kind].store(c, std::memory_order_relaxed);
     }
     return c;
 }
