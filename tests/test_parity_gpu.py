@@ -188,6 +188,22 @@ def test_transpose_plan(mk, cuda, path):
 
 
 @pytest.mark.parametrize("path", CASES, ids=IDS)
+def test_dense_plan(mk, cuda, path):
+    """The dense backward's plan: the transpose plus, per CSC slot, the CSR row of its edge and
+    its weight (maxk_dense_plan), checked against numpy."""
+    z = load_golden(path)
+    V = z["row_ptr"].size - 1
+    col_ptr, t_src, t_w = mk.dense_plan(T(z["row_ptr"], cuda), T(z["col_idx"], cuda),
+                                        T(z["val"], cuda), V, cache=False)
+    order = np.argsort(z["col_idx"], kind="stable")
+    rows = np.repeat(np.arange(V), np.diff(z["row_ptr"]))
+    tp, _, _ = O.transpose_csr(z["row_ptr"], z["col_idx"], z["val"])
+    assert np.array_equal(col_ptr.cpu().numpy(), tp)
+    assert np.array_equal(t_src.cpu().numpy(), rows[order])
+    assert np.array_equal(t_w.cpu().numpy(), z["val"][order])
+
+
+@pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_bucket_plan(mk, cuda, path):
     """Per bucket of 2^shift columns: the CSR edge ids whose column lies in it, in CSR order,
     and the column inside the bucket (checked against numpy)."""
