@@ -733,12 +733,26 @@ int fwd_resident_waves(int kg, int DS, int per_simd) {
     return by_lds < by_vgpr ? by_lds : by_vgpr;
 }
 
+// Long rows (a dense graph, e.g. a Reddit-sized graph's vertex-range shard: 14.4M tokens at
+// N = 8, rows of ~490 edges): items of at least two average rows (at most 1024 tokens), so most
+// rows are walked whole instead of split into slabs (that shard's forward at 256 / 512 / 1024 /
+// 2048 tokens: 0.256 / 0.237 / 0.237 / 0.254 ms; the N = 4 shard at 438 / 1024: 0.449 / 0.440;
+// profiles/r05/tune/fwd_chunk_shards/) -- while the items still fill every wave slot (a small
+// dense graph keeps the one-round sizing below)
+int64_t fwd_long_rows(int64_t num_rows, int64_t num_e, int64_t c, int resident) {
+    if (num_rows <= 0 || num_e < kFwdSparseDegree * num_rows) return c;
+    const int64_t two_rows = (2 * ceil_div(num_e, num_rows) + 63) / 64 * 64;
+    const int64_t want = two_rows < 1024 ? two_rows : 1024;
+    if (c >= want || (num_rows + num_e) / want < 256LL * resident) return c;
+    return want;
+}
+
 int fwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int resident) {
     if (chunk > 0) return chunk;
     // ~8 waves of work per resident wave slot on 256 CUs, within [256, 2048] tokens
     const int64_t total = num_rows + num_e;
     int64_t c = ceil_div(total, 256LL * 32 * 8);
-    if (c >= 256) return (int)(c > 2048 ? 2048 : c);
+    if (c >= 256) return (int)fwd_long_rows(num_rows, num_e, c > 2048 ? 2048 : c, resident);
     // A smaller graph has fewer items than wave slots at 256 tokens: size the items so all of
     // them are resident in one round (90 % of the slots, for uneven block placement), since each
     // wave is a chain of dependent gathers and a second round costs a whole item's latency.
@@ -746,7 +760,7 @@ int fwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int resident) {
     // 144 / 160 / 176 / 192 / 256 tokens takes 0.0527 / 0.049 / 0.051 / 0.053 / 0.0585 ms
     // (profiles/r04/tune/flickr_chunk_sweep.txt).
     c = ceil_div(total * 10, 256LL * resident * 9);
-    return (int)(c < 64 ? 64 : (c > 256 ? 256 : c));
+    return (int)fwd_long_rows(num_rows, num_e, c < 64 ? 64 : (c > 256 ? 256 : c), resident);
 }
 
 // LDS row stride per copy: D padded to 16 B, plus one 16-B group holding the

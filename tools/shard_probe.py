@@ -26,6 +26,8 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--reorder", action="store_true", help="relabel by maxk_graph.locality_order")
 ap.add_argument("--pipelines", type=int, nargs="*", default=[],
                 help="also time the pipelined gather mode's column parts (maxk_dist PIPELINE)")
+ap.add_argument("--chunks", type=int, nargs="*", default=[],
+                help="also time rank 0's forward at these item sizes (0 = the automatic one)")
 ap.add_argument("--busbw", type=float, nargs="*", default=[250.0, 375.0, 500.0],
                 help="RCCL all-gather / reduce-scatter bus bandwidths (GB/s) for the step model")
 a = ap.parse_args()
@@ -78,6 +80,14 @@ for world in a.worlds:
                             (sh.row_ptr, sh.col_idx))
         tf = timed(lambda: mk.spgemm_forward(sh.row_ptr, sh.col_idx, sh.values, cv_all, ci_all, D,
                                              out=y, validate=False))
+        if a.chunks and rank == 0:
+            line = []
+            for c in a.chunks:
+                tc = timed(lambda: mk.spgemm_forward(sh.row_ptr, sh.col_idx, sh.values, cv_all,
+                                                     ci_all, D, out=y, validate=False, chunk=c))
+                line.append(f"{c}: {tc:.3f}")
+            print(f"  N={world} rank 0 forward by item size (tokens: ms): " + ", ".join(line),
+                  flush=True)
         tb = timed(lambda: mk.sspmm_backward(sh.row_ptr, sh.col_idx, sh.values, gl, ci_all,
                                              out=gs, validate=False, mode=mode, plan=plan))
         if tf + tb > worst[0] + worst[1]:
