@@ -164,6 +164,48 @@ def topk(x, k):
     return val, idx
 
 
+def topk_u8_reference(x, k):
+    """The reference's uint8 top-k kernel per row, kernels/maxk_kernel.cu:21-90 (behind
+    cuda_topk_maxk, cuda_kernel_bindings.cpp:164-201), restated in numpy; rows of 256 bytes.
+    Threshold (:30-52): 8 bisection steps, count = #(bytes > mid); count < k: high = mid, else
+    low = mid; mid = (low + high) // 2.  Selection (:56-80): for each 32-column step (column
+    32 ext + lane), the bytes > mid go to slot total + (picks of lower lanes in the step) while
+    that is < k; then total += lane 31's exclusive prefix (:77-79: lane 31 adds its own `loc`,
+    which leaves its own pick out, so the next step's first pick overwrites it); stop once
+    total >= k (:58-61).  Slots never written stay 0 (torch::zeros, :175-176).  The kernel's
+    block-level write-out (:84-89) copies 16 rows x 32 bytes per block, i.e. it is right at
+    k = 32; this restates the per-row result at every k.  Parity unpinned against the CUDA
+    kernel itself (it cannot run here); the GPU test checks the HIP restatement against this."""
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    V, D = x.shape
+    if D != 256:
+        raise ValueError("rows of 256 bytes")
+    val = np.zeros((V, k), dtype=np.uint8)
+    idx = np.zeros((V, k), dtype=np.uint8)
+    for r in range(V):
+        row = x[r].astype(np.int64)
+        low, high, mid = 0, 255, 127
+        for _ in range(8):
+            if int((row > mid).sum()) < k:
+                high = mid
+            else:
+                low = mid
+            mid = (low + high) // 2
+        total = 0
+        for ext in range(8):
+            if total >= k:
+                break
+            chunk = row[32 * ext:32 * ext + 32]
+            choose = chunk > mid
+            loc = np.cumsum(choose) - choose
+            for lane in range(32):
+                if choose[lane] and total + loc[lane] < k:
+                    val[r, total + loc[lane]] = chunk[lane]
+                    idx[r, total + loc[lane]] = 32 * ext + lane
+            total += int(loc[31])
+    return val, idx
+
+
 def warp4(row_ptr, warp_max_nz=64):
     """warp4 schedule, kernels/generate_meta.py:30-48.  Returns int32 [W*4] (flat, as on disk)."""
     row_ptr = _c(row_ptr, np.int32)

@@ -644,6 +644,63 @@ int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, 
     return MAXK_OK;
 }
 
+// The reference's uint8 top-k as it behaves (kernels/maxk_kernel.cu:21-90, behind
+// cuda_topk_maxk / cuda_topk_maxk_float), one wave per row of 256 bytes (four per lane):
+//  * threshold: 8 bisection steps on [0, 255] -- count the bytes > mid (ballots); fewer than k:
+//    high = mid, else low = mid; mid = (low + high) / 2;
+//  * selection: the bytes strictly above mid in ascending column order, 32 columns per step
+//    (column 32 s + l on lane l), at most k; the step's count is the exclusive prefix of its
+//    lane 31, so a pick in column 32 s + 31 is overwritten by the next step's first pick, as in
+//    the reference; slots never filled stay 0 (its torch::zeros outputs).
+// The row's output is assembled in LDS (the overwrite order kept) and stored once.
+__global__ __launch_bounds__(kBlock) void topk_u8_reference_kernel(const uint8_t *__restrict__ x,
+                                                                   uint8_t *__restrict__ val,
+                                                                   uint8_t *__restrict__ idx,
+                                                                   int num_rows, int k) {
+    __shared__ uint8_t s_out[kWavesPerBlock][2 * 256];
+    const int wid = threadIdx.x / kWave;
+    const int lane = lane_id();
+    uint8_t *sv = s_out[wid], *si = s_out[wid] + 256;
+    for (int row = blockIdx.x * kWavesPerBlock + wid; row < num_rows;
+         row += gridDim.x * kWavesPerBlock) {
+        const uint32_t w = reinterpret_cast<const uint32_t *>(x + (int64_t)row * 256)[lane];
+        int low = 0, high = 255, mid = 127;
+        for (int it = 0; it < 8; ++it) {
+            int count = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                count += __popcll(__ballot((int)((w >> (8 * b)) & 255u) > mid));
+            if (count < k)
+                high = mid;
+            else
+                low = mid;
+            mid = (low + high) / 2;
+        }
+        for (int i = lane; i < 2 * k; i += kWave) s_out[wid][i < k ? i : 256 + i - k] = 0;
+        wave_lds_fence();
+        int total = 0;
+        for (int ext = 0; ext < 8 && total < k; ++ext) {
+            const int c = ext * 32 + (lane & 31);  // lanes 32..63 mirror 0..31 and do not pick
+            const uint32_t src = (uint32_t)__shfl((int)w, c >> 2);
+            const int v = (int)((src >> (8 * (c & 3))) & 255u);
+            const bool choose = lane < 32 && v > mid;
+            const uint64_t mask = __ballot(choose);
+            const int loc = __popcll(mask & ((1ull << lane) - 1));
+            if (choose && total + loc < k) {
+                sv[total + loc] = (uint8_t)v;
+                si[total + loc] = (uint8_t)c;
+            }
+            wave_lds_fence();
+            total += __popcll(mask & 0x7fffffffull);  // lane 31's exclusive prefix
+        }
+        for (int i = lane; i < k; i += kWave) {
+            val[(int64_t)row * k + i] = sv[i];
+            idx[(int64_t)row * k + i] = si[i];
+        }
+        wave_lds_fence();
+    }
+}
+
 }  // namespace
 }  // namespace maxk
 
@@ -725,4 +782,23 @@ extern "C" int maxk_cbsr_scatter_dense(const float *cbsr_val, const uint8_t *cbs
     clear_error();
     MAXK_REQUIRE(num_rows == 0 || cbsr_val, "cbsr_val must not be NULL");
     return scatter_launch(cbsr_val, cbsr_idx, nullptr, dense, num_rows, dim_origin, dim_k, stream);
+}
+
+extern "C" int maxk_topk_u8_reference(const uint8_t *x, uint8_t *val, uint8_t *idx,
+                                      int64_t num_rows, int32_t dim_origin, int32_t dim_k,
+                                      void *stream) {
+    clear_error();
+    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
+    MAXK_REQUIRE(dim_origin == 256, "the reference's uint8 top-k has rows of 256, got %d",
+                 dim_origin);
+    MAXK_REQUIRE(dim_k >= 1 && dim_k <= 256, "dim_k must be in [1,256], got %d", dim_k);
+    if (num_rows == 0) return MAXK_OK;
+    MAXK_REQUIRE(x && val && idx, "pointers must not be NULL");
+    MAXK_REQUIRE(((uintptr_t)x & 3) == 0, "x must be 4-B aligned");
+    const int64_t blocks = ceil_div(num_rows, kWavesPerBlock);
+    hipLaunchKernelGGL(topk_u8_reference_kernel,
+                       dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(kBlock), 0,
+                       as_stream(stream), x, val, idx, (int)num_rows, dim_k);
+    MAXK_LAUNCHED("topk_u8_reference_kernel");
+    return MAXK_OK;
 }

@@ -35,6 +35,7 @@ _capi.load()  # ImportError here <=> extension missing (callers test this, like 
 
 __all__ = [
     "spmm_maxk_forward", "spmm_maxk_backward", "cuda_topk_maxk", "cuda_topk_maxk_float",
+    "topk_u8_reference",
     "prepare_cbsr_format_maxk", "cusparse_spmm", "load_warp4_metadata",
     "load_warp4_metadata_csc", "generate_sparse_selector", "benchmark_spmm_maxk",
     "validate_spmm_maxk", "validate_spmm_maxk_backward", "CudaTimer",
@@ -1095,17 +1096,56 @@ def _check_topk_rows(dev, name):
         raise RuntimeError(f"{name}: {bad} rows took other than k winners (kernel bug)")
 
 
-def cuda_topk_maxk(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """uint8 top-k (cuda_kernel_bindings.cpp:164-201): (values u8 [N,k], indices u8 [N,k])."""
+def topk_u8_reference(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The reference's uint8 top-k kernel as it behaves (maxk_topk_u8_reference; rows of 256
+    bytes): (values u8 [N,k], indices u8 [N,k]) -- bytes above an 8-step bisection threshold in
+    ascending column order, its lane-31 overwrite and zero-filled slots included."""
+    _need(input, "input", torch.uint8)
+    if input.dim() != 2 or input.shape[1] != 256:
+        raise RuntimeError("the reference's uint8 top-k takes [N, 256] rows")
+    if not 0 < k <= 256:
+        raise RuntimeError("Invalid k value")
+    N = input.shape[0]
+    val = torch.empty(N, k, dtype=torch.uint8, device=input.device)
+    idx = torch.empty(N, k, dtype=torch.uint8, device=input.device)
+    with _on(input.device):
+        _capi.check(_lib().maxk_topk_u8_reference(_ptr(input), _ptr(val), _ptr(idx), N, 256, int(k),
+                                                  _stream(input.device)), "maxk_topk_u8_reference")
+    return val, idx
+
+
+def cuda_topk_maxk(input: torch.Tensor, k: int,
+                   reference_compat: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """uint8 top-k (cuda_kernel_bindings.cpp:164-201): (values u8 [N,k], indices u8 [N,k]).
+    Exact torch.topk order by default; reference_compat=True reproduces the reference kernel's
+    own convention (topk_u8_reference: threshold bisection, ascending columns, rows of 256)."""
     if input.dtype != torch.uint8:
         raise RuntimeError("Input must be uint8 tensor")
+    if reference_compat:
+        return topk_u8_reference(input, k)
     return topk_cbsr(input, k)
 
 
-def cuda_topk_maxk_float(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(values, int32 indices) (cuda_kernel_bindings.cpp:203-238), exact (no uint8 quantisation)."""
-    val, _, idx32 = topk_cbsr(input, k, with_int32=True)
-    return val, idx32
+def cuda_topk_maxk_float(input: torch.Tensor, k: int,
+                         reference_compat: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(values, int32 indices) (cuda_kernel_bindings.cpp:203-238), exact (no uint8 quantisation)
+    by default.  reference_compat=True follows the reference binding: float input quantised to
+    clamp(round(x * 255), 0, 255) as uint8, the reference kernel's top-k on that
+    (topk_u8_reference), values returned as float / 255; uint8 input passes through."""
+    if not reference_compat:
+        val, _, idx32 = topk_cbsr(input, k, with_int32=True)
+        return val, idx32
+    if input.dtype == torch.float32:
+        q = torch.clamp((input * 255.0).round(), 0, 255).to(torch.uint8)
+        v8, i8 = topk_u8_reference(q.contiguous(), k)
+        # byte / 255 correctly rounded (the device divide may be off by an ulp): a 256-entry
+        # table divided on the host
+        table = (torch.arange(256, dtype=torch.float32) / 255.0).to(input.device)
+        return table[v8.long()], i8.to(torch.int32)
+    if input.dtype == torch.uint8:
+        v8, i8 = topk_u8_reference(input, k)
+        return v8, i8.to(torch.int32)
+    raise RuntimeError("Input must be float32 or uint8")
 
 
 def prepare_cbsr_format_maxk(features: torch.Tensor, maxk: int):

@@ -101,6 +101,7 @@ SIGNATURES = {
                                                   _p]),
     "maxk_topk_cbsr": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_u8": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),
+    "maxk_topk_u8_reference": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_error_rows": (ctypes.c_int, [_p, _i32, _p]),
     "maxk_cbsr_scatter_dense": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),
     "maxk_topk_cbsr_dense": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i32, _i32, _p]),

@@ -112,3 +112,17 @@ def test_topk_tail_fixture_pins_the_oracle():
         assert np.array_equal(v, z[f"val_k{k}"]) and np.array_equal(i, z[f"idx_k{k}"])
         order = np.argsort(-z["x"], axis=1, kind="stable")[:, :k]
         assert np.array_equal(order.astype(np.uint8), i)
+
+
+def test_topk_u8_reference_restatement():
+    """The reference's uint8 top-k, by hand on one row (kernels/maxk_kernel.cu:21-90): the
+    threshold after 8 bisection steps is 179 for k = 4; the picks > 179 in ascending columns are
+    3, 31, 40, 63, but the pick in column 31 (lane 31 of the first 32-column step) is not
+    counted and is overwritten by the next step's first pick (column 40); the last slot stays
+    0."""
+    x = np.zeros((2, 256), np.uint8)
+    x[0, [3, 31, 40, 63, 100]] = [200, 250, 180, 220, 90]
+    x[1, :] = np.arange(256)[::-1]  # 255 .. 0: the first k columns are the largest
+    v, i = O.topk_u8_reference(x, 4)
+    assert v[0].tolist() == [200, 180, 220, 0] and i[0].tolist() == [3, 40, 63, 0]
+    assert i[1].tolist() == [0, 1, 2, 3] and v[1].tolist() == [255, 254, 253, 252]

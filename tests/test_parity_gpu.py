@@ -260,6 +260,28 @@ def test_bsort_plan(mk, cuda, path):
 
 
 @pytest.mark.filterwarnings("ignore:backward mode 'bsort'")
+@pytest.mark.parametrize("k", [1, 8, 16, 32, 64, 100, 256])
+def test_topk_u8_reference_convention(mk, cuda, k):
+    """cuda_topk_maxk(reference_compat=True): the reference uint8 kernel's own convention
+    (threshold bisection, ascending columns, the lane-31 overwrite, zero-filled slots) against
+    the oracle's restatement, on uint8 rows with many ties, rows of few distinct values and a
+    row of all equal bytes; and the float binding's quantisation round(x * 255)."""
+    rng = np.random.default_rng(1000 + k)
+    x = rng.integers(0, 256, (700, 256)).astype(np.uint8)
+    x[:100] = rng.integers(0, 4, (100, 256)).astype(np.uint8) * 60   # 4 values, heavy ties
+    x[100] = 77
+    x[101, 31::32] = 255  # every step's lane-31 column the largest
+    v, i = mk.cuda_topk_maxk(T(x, cuda), k, reference_compat=True)
+    vo, io = O.topk_u8_reference(x, k)
+    assert np.array_equal(v.cpu().numpy(), vo) and np.array_equal(i.cpu().numpy(), io)
+    xf = rng.random((300, 256), dtype=np.float32) * 1.2 - 0.1
+    vf, i32 = mk.cuda_topk_maxk_float(T(xf, cuda), k, reference_compat=True)
+    q = np.clip(np.round(xf.astype(np.float32) * np.float32(255.0)), 0, 255).astype(np.uint8)
+    vq, iq = O.topk_u8_reference(q, k)
+    assert np.array_equal(i32.cpu().numpy(), iq.astype(np.int32))
+    assert np.array_equal(vf.cpu().numpy(), vq.astype(np.float32) / np.float32(255.0))
+
+
 @pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 256])
 def test_bsort_windows_against_oracle(mk, cuda, k):
     """Window-sorted backward on a products-like graph of many windows (hub rows cut by window
