@@ -852,6 +852,54 @@ def test_forward_small_sparse_paths(mk, cuda, D, k):
             assert torch.equal(gs, again)
 
 
+@pytest.mark.parametrize("D,k", [(256, 32), (128, 24), (100, 28), (256, 28)])
+def test_forward_stream_wide_records(mk, cuda, D, k):
+    """The streaming forward over records past one 128-B line (k >= 22, sparse graph), clean
+    and dirty CBSR (a repeated selector, a selector >= D) against the oracle, with hub rows split
+    over items (chunk 40), rows past the lane groups' limit, accumulate and 4-B (not 16-B)
+    aligned values; an extra dirty vertex that no edge reads changes nothing, bitwise.  (r05
+    measured reading the caller's arrays instead of records here, guarded by a device check,
+    and rejected it: profiles/r05/tune/split_source/.)"""
+    rng = np.random.default_rng(D * 1000 + k)
+    V = 3000
+    row_ptr, col = rand_graph(rng, V, 9, hubs=((7, 900), (11, 70), (1500, 130)), empty=40)
+    val = rng.random(col.size, dtype=np.float32)
+    cv = rng.standard_normal((V, k)).astype(np.float32)
+    ci = np.stack([rng.choice(D, k, replace=False) for _ in range(V)]).astype(np.uint8)
+    div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+    args = (T(row_ptr, cuda), T(col, cuda), T(val, cuda))
+
+    def fwd(cvv, civ, **kw):
+        return mk.spgemm_forward(*args, T(cvv, cuda) if isinstance(cvv, np.ndarray) else cvv,
+                                 T(civ, cuda) if isinstance(civ, np.ndarray) else civ, D,
+                                 row_div=T(div, cuda), validate=False, **kw)
+
+    yo = O.spgemm_fwd(row_ptr, col, val, cv, ci, 256, row_div=div)[:, :D]
+    for chunk in (0, 40):
+        y = fwd(cv, ci, chunk=chunk)
+        close(y, yo)
+        # one more vertex, with a repeated selector, that no edge reads
+        cvx = np.concatenate([cv, cv[:1]])
+        cix = np.concatenate([ci, ci[:1]])
+        cix[-1, 1] = cix[-1, 0]
+        assert torch.equal(fwd(cvx, cix, chunk=chunk), y)
+        acc = torch.ones(V, D, device=cuda)
+        fwd(cv, ci, chunk=chunk, out=acc, accumulate=True)
+        close(acc, yo + 1.0)
+    fv = torch.empty(V * k + 1, device=cuda)[1:].view(V, k)  # 4-B, not 16-B aligned
+    fv.copy_(T(cv, cuda))
+    close(fwd(fv, ci), yo)
+    # dirty inputs: repeated selectors sum, selectors >= D contribute nothing
+    cid = ci.copy()
+    dup = rng.choice(V, 60, replace=False)
+    cid[dup, -1] = cid[dup, 0]
+    if D < 256:
+        cid[rng.choice(V, 60, replace=False), 1] = rng.integers(D, 256, 60).astype(np.uint8)
+    yd = O.spgemm_fwd(row_ptr, col, val, cv, cid, 256, row_div=div)[:, :D]
+    for chunk in (0, 40):
+        close(fwd(cv, cid, chunk=chunk), yd)
+
+
 @pytest.mark.parametrize("k", [4, 12, 16, 32])
 def test_forward_pack_aligned_and_not(mk, cuda, k):
     """The forward's record pack runs four l per thread (cbsr_pack4_kernel) on aligned CBSR
