@@ -174,6 +174,9 @@ constexpr size_t kInfinityCacheBytes = 256ull << 20;  // MI355X MALL (MI355X_MIC
 #ifndef MAXK_DENSE_PICK  // the dense backward below k = D / 2: selected columns per lane
 #define MAXK_DENSE_PICK 1   // (pick_rows_kernel); 0 = dense rows and a selecting store
 #endif
+#ifndef MAXK_DENSE_PICK_DMAX  // the automatic mode takes the pick form on small graphs of D at
+#define MAXK_DENSE_PICK_DMAX 64  // most this, k >= D / 4 (0 = never)
+#endif
 #ifndef MAXK_DENSE_WAVES  // dense_rows_kernel: resident waves per CU its item size assumes
 #define MAXK_DENSE_WAVES 24
 #endif
@@ -241,6 +244,7 @@ int zero_words(void *p, int64_t n, hipStream_t s);
 
 // Dense route (dense_route.hip): whether (D, k) takes it, and the forward through it
 bool dense_route(int D, int k);
+bool dense_pick(int D, int k);  // the dense backward's selected-column form below k = D / 2
 size_t dense_forward_workspace_size(int64_t num_rows, int64_t num_cols, int64_t num_e, int D,
                                     int chunk);
 int dense_forward(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,

@@ -663,8 +663,6 @@ struct DenseLayout {
 
 // x_rows: rows of the dense table the route writes (forward: num_cols source rows of X;
 // backward: num_cols destination rows of Y)
-// the backward picks selected columns (pick_rows_kernel) below k = D / 2 (MAXK_DENSE_PICK)
-bool dense_pick(int D, int k) { return MAXK_DENSE_PICK && 2 * k < D && k <= kWave; }
 
 // kind as rows_blocks_per_cu; width: floats per slab row (D, or k for the pick)
 DenseLayout dense_layout(int64_t rows, int64_t x_rows, int64_t num_e, int D, int chunk, int kind,
@@ -720,6 +718,9 @@ int launch_dense_rows(const DenseLayout &L, hipStream_t s, const int32_t *ptr, c
 }
 
 }  // namespace
+
+// the backward picks selected columns (pick_rows_kernel) below k = D / 2 (MAXK_DENSE_PICK)
+bool dense_pick(int D, int k) { return MAXK_DENSE_PICK && 2 * k < D && k <= kWave; }
 
 bool dense_route(int D, int k) {
     return MAXK_DENSE_ROUTE && D % 4 == 0 && D <= MAXK_DENSE_DMAX && k % 4 == 0 && 2 * k >= D;

@@ -378,6 +378,14 @@ extern "C" int maxk_backward_mode_auto(int64_t num_rows, int64_t num_cols, int64
     // stay cache-resident (64 MiB) however sparse the graph
     const bool dense = (double)num_e * (double)(1LL << shift) >= (double)rows * (double)num_cols / 2;
     const bool small = dim_origin > 0 && (double)rows * dim_origin * 4 <= (double)(64 << 20);
+    // a small, narrow G (D <= MAXK_DENSE_PICK_DMAX, cache-resident) of a sparse graph (the
+    // pull's tiles share no source rows) at D / 4 <= k < D / 2: the
+    // dense backward's selected-column form (pick_rows_kernel) -- Flickr-sized (configs[0]),
+    // k = 16: 0.0561 against 0.0587-0.0588 ms for the pull; at k = 8 the pull stays (0.049
+    // against 0.051-0.053; profiles/r05/tune/dense_pick/)
+    if (small && !dense && dim_origin <= MAXK_DENSE_PICK_DMAX && 4 * k >= dim_origin && k % 4 == 0 &&
+        dim_origin % 4 == 0 && dense_pick(dim_origin, k))
+        return MAXK_BWD_DENSE;
     if ((dense || small) && rows <= 256LL * 65536) return MAXK_BWD_PULL;
     if (dense && k <= 16 && k % 4 == 0) return MAXK_BWD_BUCKET;
     if (k % 4 == 0 && rows <= 256LL * 65536 && num_e > 0 && pull_locality >= MAXK_HYBRID_LOCALITY)

@@ -181,7 +181,7 @@ def test_backward_mode_resolution():
     # a small gradient (Flickr, 23 MB) stays cache-resident: pull however sparse the graph
     flickr = dict(num_e=989_006, num_cols=89_250, num_rows=89_250)
     assert mk._bwd_mode("auto", 16, **flickr) == "csc"
-    assert mk._bwd_mode("auto", 16, **flickr, dim=64) == "pull"
+    assert mk._bwd_mode("auto", 16, **flickr, dim=128) == "pull"
     assert mk._bwd_mode("auto", 10, **flickr, dim=64) == "pull"
     assert mk._bwd_mode("auto", 16, **flickr, dim=9) == "csc"
     assert mk._bwd_mode("auto", 12, **reddit) == "pull"
@@ -223,7 +223,12 @@ def test_backward_mode_resolution():
         mk._bwd_mode("dense", 16, **reddit, dim=9)
     assert mk._bwd_mode("auto", 32, **flickr, dim=64) == "dense"
     assert mk._bwd_mode("auto", 64, **flickr, dim=64) == "dense"
-    assert mk._bwd_mode("auto", 28, **flickr, dim=64) == "pull"
+    # small narrow graphs at D / 4 <= k < D / 2: the dense backward's pick form (r05)
+    assert mk._bwd_mode("auto", 28, **flickr, dim=64) == "dense"
+    assert mk._bwd_mode("auto", 16, **flickr, dim=64) == "dense"
+    assert mk._bwd_mode("auto", 8, **flickr, dim=64) == "pull"
+    assert mk._bwd_mode("auto", 16, **flickr, dim=128) == "pull"
+    assert mk._bwd_mode("auto", 16, **reddit, dim=64) == "pull"  # a dense graph keeps the pull
     assert mk._bwd_mode("auto", 64, **reddit, dim=128) == "dense"
     assert mk._bwd_mode("auto", 128, **reddit, dim=256) != "dense"  # past MAXK_DENSE_DMAX
     F = (flickr["num_rows"], flickr["num_cols"], flickr["num_e"])

@@ -39,7 +39,8 @@ CONFIGS = [("reddit", 256, 8, "auto", "pull"), ("reddit", 256, 16, "auto", "pull
            ("products", 256, 8, "stream", "bsort"), ("products", 256, 16, "stream", "csc"),
            ("products", 256, 32, "auto", "csc"), ("products", 256, 64, "auto", "csc"),
            ("products_comm_ordered", 256, 32, "auto", "hybrid"),
-           ("proteins", 256, 64, "auto", "pull"), ("flickr", 64, 16, "auto", "pull")]
+           ("proteins", 256, 64, "auto", "pull"), ("flickr", 64, 16, "auto", "dense"),
+           ("flickr", 64, 8, "auto", "pull")]
 _GRAPHS = {}
 
 
