@@ -367,7 +367,10 @@ int maxk_sspmm_backward_dense(const int32_t *col_ptr, const int32_t *t_src, cons
  * (spmm_maxk_backward.cu:15-121, launched by cuda_kernel_wrappers.cu:58-76).
  *
  * maxk_backward_mode_auto: the backward a graph should use (pure host arithmetic):
- *   MAXK_BWD_DENSE where maxk_dense_route(dim_origin, dim_k); else MAXK_BWD_PULL where dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and the graph has at
+ *   MAXK_BWD_DENSE where maxk_dense_route(dim_origin, dim_k), or (its selected-column form)
+ *   for a G of at most 64 MiB on a graph below the pull's density test at dim_origin <= 64,
+ *   dim_origin / 4 <= dim_k < dim_origin / 2, both % 4 == 0; else MAXK_BWD_PULL where
+ *   dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and the graph has at
  *   least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(dim_k) columns) or a G of at
  *   most 64 MiB; else MAXK_BWD_BUCKET on such a dense graph at dim_k <= 16; else MAXK_BWD_HYBRID
  *   when pull_locality (maxk_pull_locality at maxk_pull_shift(dim_k); < 0 = unknown) reaches
