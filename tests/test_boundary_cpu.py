@@ -106,6 +106,12 @@ def test_host_side_argument_validation():
     assert L.maxk_spgemm_forward(ctypes.c_void_p(16), None, None, None, None, None,
                                  ctypes.c_void_p(16), 10, 10, 0, 64, 16, 0, None, 0, None) == -1
     assert b"workspace" in L.maxk_last_error()
+    # the reference-convention uint8 top-k: rows of 256 bytes, 1 <= k <= 256
+    assert L.maxk_topk_u8_reference(None, None, None, 10, 128, 16, None) == -1
+    assert b"256" in L.maxk_last_error()
+    assert L.maxk_topk_u8_reference(None, None, None, 10, 256, 0, None) == -1
+    assert L.maxk_topk_u8_reference(None, None, None, 10, 256, 16, None) == -1  # NULL buffers
+    assert L.maxk_topk_u8_reference(None, None, None, 0, 256, 16, None) == 0
     # empty problems are valid no-ops
     assert L.maxk_spgemm_forward(None, None, None, None, None, None, None, 0, 0, 0, 64, 16, 0,
                                  None, 0, None) == 0
