@@ -52,9 +52,11 @@ TAG_RATE_PER_S = 256 * 2.4e9
 
 # kernels making up each op of one step (rocprofv3 names, maxk:: namespace)
 OP_KERNELS = {
-    # the record route, or (k >= D / 2, D <= 128) the dense route (dense_route.hip)
+    # the record route (packed or, k in [24, 32] on sparse graphs, transport records), or
+    # (k >= D / 2, D <= 128) the dense route (dense_route.hip)
     "spgemm_forward": ["spgemm_fwd_kernel", "slab_fixup_kernel<0>", "cbsr_pack4_kernel",
-                       "cbsr_pack_kernel", "cbsr_dense_kernel", "dense_rows_kernel"],
+                       "cbsr_pack_kernel", "cbsr_records_kernel", "cbsr_dense_kernel",
+                       "dense_rows_kernel"],
     "sspmm_backward_csc": ["sspmm_bwd_kernel", "csc_sum_kernel", "slab_fixup_kernel<1>"],
     # k % 4 == 0: slot-ordered selectors, quantile-slot tiles; else pull_tile_kernel; plus
     # gprime_kernel when a row_div is given (the bench passes none)

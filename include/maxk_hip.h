@@ -104,6 +104,28 @@ int maxk_spgemm_forward_accumulate_sel(const int32_t *row_ptr, const int32_t *co
                                        int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
                                        void *workspace, size_t workspace_bytes, void *stream,
                                        uint8_t *edge_sel);
+/* Transport records (the sharded forward, r05): [k f32 | k u8] per vertex at a stride of 5k bytes,
+ * the bytes a vertex-range shard all-gathers anyway, built by each owner for its own rows
+ * (maxk_cbsr_records) so the receivers walk the gathered buffer (maxk_spgemm_forward_records)
+ * with no record pack over every gathered vertex.  Selectors stay the caller's bytes; a repeated
+ * selector's first occurrence carries the sum of its values in l order and the later ones, like
+ * selectors >= dim_origin, a skip marker (a NaN payload; a kept NaN value is stored as the
+ * canonical quiet NaN) -- the same sums as maxk_spgemm_forward.  maxk_records_ok says whether
+ * the records forward applies: the streaming walker of a sparse graph (average degree < 128),
+ * dim_k % 4 == 0 in [24, 32], num_cols * 5 * dim_k < 2^32 (where the 5k-byte stride costs no
+ * extra line per gather against the packed record).  rec 4-B aligned; workspace as
+ * maxk_spgemm_forward_workspace_size; accumulate adds onto out.  Replaces the same reference
+ * kernel as maxk_spgemm_forward (spmm_maxk.cu:17-113). */
+int maxk_records_ok(int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                    int32_t dim_k);
+int maxk_cbsr_records(const float *cbsr_val, const uint8_t *cbsr_idx, uint8_t *rec,
+                      int64_t num_rows, int32_t dim_origin, int32_t dim_k, void *stream);
+int maxk_spgemm_forward_records(const int32_t *row_ptr, const int32_t *col_idx,
+                                const float *edge_val, const uint8_t *rec, const float *row_div,
+                                float *out, int64_t num_rows, int64_t num_cols, int64_t num_e,
+                                int32_t dim_origin, int32_t dim_k, int32_t chunk_edges,
+                                void *workspace, size_t workspace_bytes, void *stream,
+                                int32_t accumulate);
 
 /* ---------------------------------------------------------------------------
  * Backward outer-product sampled SpMM (SSpMM):

@@ -35,6 +35,9 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_FWD_STREAM  // forward, sparse graphs: lane groups stream rows of at most this many
 #define MAXK_FWD_STREAM 64  // edges each (stream_rows); 0 = off (the short-row batches)
 #endif
+#ifndef MAXK_FWD_RECORDS  // streaming forward, k in [24, 32]: 5k-byte transport records instead
+#define MAXK_FWD_RECORDS 1  // of the packed ones (maxk_records_ok); 0 = the packed records
+#endif
 #ifndef MAXK_FWD_WAVES
 #define MAXK_FWD_WAVES 1
 #endif

@@ -193,6 +193,77 @@ __global__ __launch_bounds__(kPackBlock) void cbsr_pack4_kernel(const float *__r
     }
 }
 
+// Transport records (r05, maxk_cbsr_records / maxk_spgemm_forward_records): [k f32 | k u8] per
+// vertex at a stride of 5k bytes -- the bytes a sharded forward all-gathers anyway -- so owners
+// build them for their own rows before the exchange and receivers walk the gathered buffer with
+// no pack over every gathered vertex.  The selectors stay the caller's bytes (the backward reads
+// them); a repeated selector's first occurrence carries the sum of its values in l order and
+// the later ones, and any selector >= D, carry kRecSkip (a NaN payload the walkers send to the
+// trash column); a NaN value the caller kept is stored as the canonical quiet NaN, so kRecSkip
+// never stands for a kept value.  One thread per (vertex, four l), k % 4 == 0.
+constexpr uint32_t kRecSkip = 0x7fbadbadu;
+__global__ __launch_bounds__(kPackBlock) void cbsr_records_kernel(const float *__restrict__ cbsr_val,
+                                                                  const uint8_t *__restrict__ cbsr_idx,
+                                                                  uint8_t *__restrict__ rec,
+                                                                  int num_rows, int k, int D) {
+    __shared__ uint32_t s_bits[kPackBlock * 8];
+    __shared__ int s_dup[kPackBlock];
+    const int tpv = k >> 2;
+    const int vpw = kPackBlock / tpv;
+    const int t = threadIdx.x;
+    const int vl = t / tpv, l0 = (t - vl * tpv) * 4;
+    const int RS = 5 * k;
+    for (int64_t g0 = (int64_t)blockIdx.x * vpw; g0 < num_rows; g0 += (int64_t)gridDim.x * vpw) {
+        const int64_t v = g0 + vl;
+        const bool act = vl < vpw && v < num_rows;
+        for (int i = t; i < vpw * 8; i += kPackBlock) s_bits[i] = 0u;
+        if (t < vpw) s_dup[t] = 0;
+        __syncthreads();
+        uint32_t w = 0u;
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+        if (act) {
+            const uint8_t *ci = cbsr_idx + v * k;
+            const float *cv = cbsr_val + v * k;
+            w = (uint32_t)ci[l0] | ((uint32_t)ci[l0 + 1] << 8) | ((uint32_t)ci[l0 + 2] << 16) |
+                ((uint32_t)ci[l0 + 3] << 24);
+            uint32_t bad = 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[j] = cv[l0 + j];
+                const uint32_t sj = (w >> (8 * j)) & 255u;
+                const uint32_t old = atomicOr(&s_bits[vl * 8 + (sj >> 5)], 1u << (sj & 31));
+                bad |= ((old >> (sj & 31)) & 1u) | (sj >= (uint32_t)D ? 1u : 0u);
+            }
+            if (bad) s_dup[vl] = 1;
+        }
+        __syncthreads();
+        if (act) {
+            const bool any = s_dup[vl] != 0;
+            uint8_t *p = rec + v * RS;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t sj = (w >> (8 * j)) & 255u;
+                float x = o[j];
+                bool keep = sj < (uint32_t)D;
+                if (any) {  // rare: the pack's rule (the first occurrence sums, in l order)
+                    const int l = l0 + j;
+                    const uint8_t *ci = cbsr_idx + v * k;
+                    const float *cv = cbsr_val + v * k;
+                    for (int m = 0; m < l; ++m) keep = keep && ci[m] != sj;
+                    if (keep)
+                        for (int m = l + 1; m < k; ++m)
+                            if (ci[m] == sj) x += cv[m];
+                }
+                const uint32_t xb = __float_as_uint(x);
+                const uint32_t ob = !keep ? kRecSkip : (x != x ? 0x7fc00000u : xb);
+                reinterpret_cast<uint32_t *>(p)[l0 + j] = ob;
+            }
+            *reinterpret_cast<uint32_t *>(p + 4 * k + l0) = w;
+        }
+        __syncthreads();
+    }
+}
+
 // EMIT (maxk_spgemm_forward_sel, k <= KG so one pass over l): every lane stores its edge's
 // selector byte to esel[e * k + l] -- a wave step's G edges x k bytes are one contiguous run.
 // The stores go one batch late, right after the next batch's column loads and before that
@@ -458,6 +529,55 @@ struct PackedSrc {
         return min(s, trash);
     }
 };
+// Transport records (cbsr_records_kernel): value at c*5k + 4l, selector byte at c*5k + 4k + l;
+// kRecSkip values and selectors >= D go to the trash column.
+struct RecordSrc {
+    __amdgpu_buffer_rsrc_t rrs;
+    uint32_t vo, so, RS;
+    __device__ __forceinline__ void load(int c, float &v, int &s) const {
+        const uint32_t ro = __umul24((uint32_t)c, RS);
+        const uint32_t vb = __builtin_amdgcn_raw_buffer_load_b32(rrs, (int)(ro + vo), 0, 0);
+        const int sb = __builtin_amdgcn_raw_buffer_load_b8(rrs, (int)(ro + so), 0, 0);
+        v = __uint_as_float(vb);
+        s = vb == kRecSkip ? 0x100 : sb;  // 0x100 >= any D: the trash column
+    }
+    __device__ __forceinline__ int col(int s, int D, int trash) const {
+        return s < D ? s : trash;
+    }
+};
+
+// EdgeWalker::run's single-pass buffer path (KG >= k, no selector stream) over a source: the
+// transport-record walks of hub-row pieces and of rows longer than the streaming groups take.
+template <int KG, int U, class Src>
+__device__ __forceinline__ void walk_src(float *acc_g, const int32_t *__restrict__ col_idx,
+                                         const float *__restrict__ edge_val, const Src &src,
+                                         int sb, int se, int D, int trash, bool lok, int lane) {
+    constexpr int G = kWave / KG;
+    const int grp = lane / KG;
+    const int n = se - sb;  // wave-uniform
+    const auto crs = wave_buffer(col_idx + sb, (uint32_t)n * 4u);
+    const auto vrs = wave_buffer(edge_val + sb, (uint32_t)n * 4u);
+    for (int base = 0; base < n; base += G * U) {
+        int c[U];
+        float w[U];
+        const int lo = (base + grp) * 4;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            c[u] = (int)__builtin_amdgcn_raw_buffer_load_b32(crs, lo + u * G * 4, 0, 0);
+            w[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vrs, lo + u * G * 4, 0, 0));
+        }
+        float v[U];
+        int s[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) src.load(c[u], v[u], s[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool live = lok && base + u * G + grp < n;
+            float *a = &acc_g[live ? src.col(s[u], D, trash) : trash];
+            *a = __builtin_fmaf(w[u], v[u], *a);  // one rounding, in every variant
+        }
+    }
+}
 // four consecutive copy columns, zeroed as they are read
 __device__ __forceinline__ float4 acc_take4(float *a) {
     const float4 x = *reinterpret_cast<float4 *>(a);
@@ -598,9 +718,11 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
     const float *__restrict__ edge_val, const uint8_t *__restrict__ rec, int RS,
     const float *__restrict__ row_div, float *__restrict__ out, float *__restrict__ slab,
     int32_t *__restrict__ slab_row, int num_rows, int64_t num_e, int D, int DS, int k,
-    int chunk, int n_items, int accumulate, uint8_t *__restrict__ esel) {
+    int chunk, int n_items, int accumulate, uint8_t *__restrict__ esel,
+    const uint8_t *__restrict__ trec = nullptr) {
     // accumulate: bit 0 adds onto out (maxk_spgemm_forward_accumulate), bit 1 stores the output
-    // rows non-temporally
+    // rows non-temporally.  STREAM with trec: the caller's transport records (RecordSrc, stride
+    // 5k) instead of the packed ones
     constexpr int NC = kWave / KG;  // LDS copies per wave (one per edge group)
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int wid = threadIdx.x / kWave;
@@ -614,6 +736,14 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
     for (int j = lane * 4; j < NC * DS; j += kWave * 4)
         *reinterpret_cast<float4 *>(&acc[j]) = make_float4(0.f, 0.f, 0.f, 0.f);
     float *acc_g = acc + (lane / KG) * DS;
+    const bool lok_s = lane % KG < k;
+    // built where it is used (a descriptor kept live across the kernel goes to scratch)
+    auto rec_src = [&]() {
+        const uint32_t lc = (uint32_t)(lok_s ? lane % KG : k - 1);
+        return RecordSrc{wave_buffer(trec, 0xffffffffu), 4u * lc, 4u * (uint32_t)k + lc,
+                         5u * (uint32_t)k};
+    };
+    const bool tr = STREAM && trec != nullptr;
 
     const int64_t total = (int64_t)num_rows + num_e;
     const int64_t d0 = (int64_t)item * chunk;
@@ -635,8 +765,12 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         if (sb < se && !whole) {
             const float div = row_div ? row_div[r - 1] : 1.f;  // loaded before the walk
             wave_lds_fence();
-            EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb, (int)se,
-                                               k, DS - 1, lane, esel);
+            if (tr)
+                walk_src<KG, U>(acc_g, col_idx, edge_val, rec_src(), (int)sb, (int)se, D, DS - 1,
+                                lok_s, lane);
+            else
+                EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)sb,
+                                                   (int)se, k, DS - 1, lane, esel);
             flush_row<NC>(acc, DS, slab + (int64_t)item * D, D, div, row_div != nullptr, lane);
             cont = r - 1;
         }
@@ -655,13 +789,18 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         if constexpr (STREAM) {
             // every row of at most MAXK_FWD_STREAM edges by the streaming lane groups; a longer
             // one (or the item's end) stops them, and the wave walks it below
-            const bool lok = lane % KG < k;
-            const uint32_t lc = (uint32_t)(lok ? lane % KG : k - 1);
-            const PackedSrc src{wave_buffer(rec, 0xffffffffu), 4u * lc,
-                                4u * (uint32_t)k + 2u * lc, (uint32_t)RS};
-            r = stream_rows<KG, U>(acc, DS, r, row_ptr, num_rows, d1, col_idx, edge_val, src,
-                                   row_div, out, D, k, DS - 1, lane, accumulate,
-                                   min(MAXK_FWD_STREAM, chunk), num_e);
+            if (tr) {
+                r = stream_rows<KG, U>(acc, DS, r, row_ptr, num_rows, d1, col_idx, edge_val,
+                                       rec_src(), row_div, out, D, k, DS - 1, lane, accumulate,
+                                       min(MAXK_FWD_STREAM, chunk), num_e);
+            } else {
+                const uint32_t lc = (uint32_t)(lok_s ? lane % KG : k - 1);
+                const PackedSrc src{wave_buffer(rec, 0xffffffffu), 4u * lc,
+                                    4u * (uint32_t)k + 2u * lc, (uint32_t)RS};
+                r = stream_rows<KG, U>(acc, DS, r, row_ptr, num_rows, d1, col_idx, edge_val, src,
+                                       row_div, out, D, k, DS - 1, lane, accumulate,
+                                       min(MAXK_FWD_STREAM, chunk), num_e);
+            }
             if (r >= num_rows) break;
             rb = row_ptr[r];
             if (rb + r >= d1) break;
@@ -713,7 +852,10 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         if (d1 - r - 1 < se && se - rb > chunk) se = d1 - r - 1;  // a hub row: split
         const float div = row_div ? row_div[r] : 1.f;  // loaded before the walk
         wave_lds_fence();
-        if (rb < se)
+        if (rb < se && tr)
+            walk_src<KG, U>(acc_g, col_idx, edge_val, rec_src(), (int)rb, (int)se, D, DS - 1,
+                            lok_s, lane);
+        else if (rb < se)
             EdgeWalker<KG, U, WIDE, EMIT>::run(acc_g, col_idx, edge_val, rec, RS, (int)rb, (int)se,
                                                k, DS - 1, lane, esel);
         flush_row<NC>(acc, DS, out + (int64_t)r * D, D, div, row_div != nullptr, lane,
@@ -808,7 +950,7 @@ template <int KG>
 void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const int32_t *col_idx,
                 const float *edge_val, const uint8_t *rec, const float *row_div, float *out,
                 float *slab, int32_t *slab_row, int num_rows, int64_t num_e, int D, int k,
-                int accumulate, uint8_t *esel) {
+                int accumulate, uint8_t *esel, const uint8_t *trec = nullptr) {
     constexpr int U = MAXK_FWD_U;
     constexpr int NC = kWave / KG;
     const size_t lds = (size_t)kWavesPerBlock * NC * L.DS * sizeof(float);
@@ -826,7 +968,7 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
             hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, false, true>), grid, dim3(kBlock),
                                lds, s, row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab,
                                slab_row, num_rows, num_e, D, L.DS, k, L.chunk, L.n_items,
-                               accumulate, nullptr);
+                               accumulate, nullptr, trec);
     } else if (L.deep)
         // dense graphs: 16 wave steps of loads per batch (Reddit-sized k = 16 forward 1.613 ->
         // 1.594 ms, k = 32 / 64 and ogbn-proteins 0.3-0.8 % faster; on the sparse products
@@ -866,11 +1008,20 @@ extern "C" size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t n
 }
 
 namespace {
+// the forward over transport records applies (maxk_records_ok): the streaming walker, one pass
+// over l, records past one line in the packed form (6k > 128, where a 5k-byte stride costs no
+// extra line per gather: 160 B at k = 32 spans two lines as the 256-B record does)
+bool records_ok(const FwdLayout &L, int64_t num_cols, int k) {
+    return L.stream && k % 4 == 0 && 6 * k > 128 && k <= L.kg && k <= 32 &&
+           (uint64_t)num_cols * 5u * (uint64_t)k < (1ull << 32);
+}
+
 int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_val,
                  const float *cbsr_val, const uint8_t *cbsr_idx, const float *row_div, float *out,
                  int64_t num_rows, int64_t num_cols, int64_t num_e, int32_t dim_origin,
                  int32_t dim_k, int32_t chunk_edges, void *workspace, size_t workspace_bytes,
-                 void *stream, int accumulate, uint8_t *esel = nullptr) {
+                 void *stream, int accumulate, uint8_t *esel = nullptr,
+                 const uint8_t *trec = nullptr) {
     MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range: %lld",
                  (long long)num_rows);
     MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
@@ -883,10 +1034,10 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
     MAXK_REQUIRE(num_cols * (int64_t)dim_k < (1LL << 31), "num_cols*k too large");
     if (num_rows == 0) return MAXK_OK;
     MAXK_REQUIRE(row_ptr && out, "row_ptr/out must not be NULL");
-    MAXK_REQUIRE(num_e == 0 || (col_idx && edge_val && cbsr_val && cbsr_idx),
+    MAXK_REQUIRE(num_e == 0 || (col_idx && edge_val && ((cbsr_val && cbsr_idx) || trec)),
                  "CSR/CBSR pointers must not be NULL");
     MAXK_REQUIRE(num_e == 0 || num_cols > 0, "edges present but num_cols == 0");
-    if (!esel && dense_route(dim_origin, dim_k) && ((uintptr_t)cbsr_val & 15) == 0 &&
+    if (!esel && !trec && dense_route(dim_origin, dim_k) && ((uintptr_t)cbsr_val & 15) == 0 &&
         ((uintptr_t)cbsr_idx & 3) == 0 && ((uintptr_t)out & 15) == 0) {
         // k >= D / 2: dense rows carry no more bytes than the CBSR (dense_route.hip)
         MAXK_REQUIRE(((uintptr_t)workspace & 255) == 0, "workspace must be 256-B aligned");
@@ -906,7 +1057,22 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
     int32_t *slab_row = reinterpret_cast<int32_t *>(ws + L.row_off);
     hipStream_t s = as_stream(stream);
     const int D = dim_origin, k = dim_k;
-    if (num_cols > 0 && MAXK_PACK4 && k % 4 == 0 && ((uintptr_t)cbsr_val & 15) == 0 &&
+    if (trec) {
+        MAXK_REQUIRE(records_ok(L, num_cols, k), "transport records need the streaming forward "
+                     "(a sparse graph), k %% 4 == 0 in [24, 32] and num_cols * 5k < 2^32");
+    } else if (MAXK_FWD_RECORDS && !esel && num_cols > 0 && records_ok(L, num_cols, k) &&
+               ((uintptr_t)cbsr_val & 3) == 0) {
+        // the same walk over 5k-byte records packed here (they fit the record table): the
+        // ogbn-products-sized graph at k = 32, forward 4.885 -> 4.813 ms, bitwise equal
+        // (profiles/r05/tune/transport_records/)
+        const int vpw = kPackBlock / (k / 4);
+        const int64_t groups = ceil_div(num_cols, (int64_t)vpw);
+        hipLaunchKernelGGL(cbsr_records_kernel,
+                           dim3((unsigned)(groups < MAXK_PACK_GRID ? groups : MAXK_PACK_GRID)),
+                           dim3(kPackBlock), 0, s, cbsr_val, cbsr_idx, rec, (int)num_cols, k, D);
+        MAXK_LAUNCHED("cbsr_records_kernel");
+        trec = rec;
+    } else if (num_cols > 0 && MAXK_PACK4 && k % 4 == 0 && ((uintptr_t)cbsr_val & 15) == 0 &&
         ((uintptr_t)cbsr_idx & 3) == 0) {
         const int vpw = kPackBlock / (k / 4);
         const int64_t groups = ceil_div(num_cols, (int64_t)vpw);
@@ -938,7 +1104,7 @@ int forward_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *ed
 #define MAXK_CASE(KGV)                                                                     \
     case KGV:                                                                              \
         launch_fwd<KGV>(L, s, row_ptr, col_idx, edge_val, rec, row_div, out, slab,         \
-                        slab_row, nr, num_e, D, k, flags, esel);                           \
+                        slab_row, nr, num_e, D, k, flags, esel, trec);                     \
         break;
         MAXK_CASE(8)
         MAXK_CASE(16)
@@ -1023,4 +1189,61 @@ extern "C" int maxk_spgemm_forward_accumulate(const int32_t *row_ptr, const int3
     return forward_impl(row_ptr, col_idx, edge_val, cbsr_val, cbsr_idx, row_div, out, num_rows,
                         num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
                         workspace_bytes, stream, 1);
+}
+
+extern "C" int maxk_records_ok(int64_t num_rows, int64_t num_cols, int64_t num_e,
+                               int32_t dim_origin, int32_t dim_k) {
+    if (num_rows <= 0 || num_cols <= 0 || num_e <= 0 || dim_origin <= 0 || dim_k <= 0 ||
+        dim_k > dim_origin || dim_origin > kMaxDim)
+        return 0;
+    return records_ok(fwd_layout(num_rows, num_cols, num_e, dim_origin, dim_k, 0), num_cols,
+                      dim_k)
+               ? 1
+               : 0;
+}
+
+extern "C" int maxk_cbsr_records(const float *cbsr_val, const uint8_t *cbsr_idx, uint8_t *rec,
+                                 int64_t num_rows, int32_t dim_origin, int32_t dim_k,
+                                 void *stream) {
+    clear_error();
+    MAXK_REQUIRE(num_rows >= 0 && num_rows < (1LL << 31), "num_rows out of range");
+    MAXK_REQUIRE(dim_origin >= 1 && dim_origin <= kMaxDim, "dim_origin must be in [1,256]");
+    MAXK_REQUIRE(dim_k >= 4 && dim_k <= dim_origin && dim_k % 4 == 0 && dim_k <= 128,
+                 "transport records need dim_k %% 4 == 0 in [4, min(dim_origin, 128)], got %d",
+                 dim_k);
+    if (num_rows == 0) return MAXK_OK;
+    MAXK_REQUIRE(cbsr_val && cbsr_idx && rec, "pointers must not be NULL");
+    MAXK_REQUIRE(((uintptr_t)rec & 3) == 0 && ((uintptr_t)cbsr_val & 3) == 0,
+                 "records and values must be 4-B aligned");
+    const int vpw = kPackBlock / (dim_k / 4);
+    const int64_t groups = ceil_div(num_rows, (int64_t)vpw);
+    hipLaunchKernelGGL(cbsr_records_kernel,
+                       dim3((unsigned)(groups < MAXK_PACK_GRID ? groups : MAXK_PACK_GRID)),
+                       dim3(kPackBlock), 0, as_stream(stream), cbsr_val, cbsr_idx, rec,
+                       (int)num_rows, dim_k, dim_origin);
+    MAXK_LAUNCHED("cbsr_records_kernel");
+    return MAXK_OK;
+}
+
+extern "C" int maxk_spgemm_forward_records(const int32_t *row_ptr, const int32_t *col_idx,
+                                           const float *edge_val, const uint8_t *rec,
+                                           const float *row_div, float *out, int64_t num_rows,
+                                           int64_t num_cols, int64_t num_e, int32_t dim_origin,
+                                           int32_t dim_k, int32_t chunk_edges, void *workspace,
+                                           size_t workspace_bytes, void *stream,
+                                           int32_t accumulate) {
+    clear_error();
+    if (accumulate && num_e == 0) return MAXK_OK;  // adds zeros
+    MAXK_REQUIRE(num_e == 0 || rec, "rec must not be NULL");
+    MAXK_REQUIRE(((uintptr_t)rec & 3) == 0, "records must be 4-B aligned");
+    if (num_e == 0) {  // nothing to walk: zero rows
+        MAXK_REQUIRE(num_rows >= 0 && dim_origin >= 1 && dim_origin <= kMaxDim,
+                     "num_rows / dim_origin out of range");
+        MAXK_REQUIRE(num_rows == 0 || out, "out must not be NULL");
+        return num_rows == 0 ? MAXK_OK
+                             : zero_words(out, num_rows * (int64_t)dim_origin, as_stream(stream));
+    }
+    return forward_impl(row_ptr, col_idx, edge_val, nullptr, nullptr, row_div, out, num_rows,
+                        num_cols, num_e, dim_origin, dim_k, chunk_edges, workspace,
+                        workspace_bytes, stream, accumulate ? 1 : 0, nullptr, rec);
 }

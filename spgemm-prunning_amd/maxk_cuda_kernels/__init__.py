@@ -36,6 +36,9 @@ _capi.load()  # ImportError here <=> extension missing (callers test this, like 
 __all__ = [
     "spmm_maxk_forward", "spmm_maxk_backward", "cuda_topk_maxk", "cuda_topk_maxk_float",
     "topk_u8_reference",
+    "records_ok",
+    "cbsr_records",
+    "spgemm_forward_records",
     "prepare_cbsr_format_maxk", "cusparse_spmm", "load_warp4_metadata",
     "load_warp4_metadata_csc", "generate_sparse_selector", "benchmark_spmm_maxk",
     "validate_spmm_maxk", "validate_spmm_maxk_backward", "CudaTimer",
@@ -278,6 +281,64 @@ def spgemm_forward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
             _ptr(indptr), _ptr(indices), _ptr(values), _ptr(cbsr_val), _ptr(cbsr_idx),
             _ptr(row_div), _ptr(out), num_rows, num_cols, E, D, k, chunk, _ptr(ws), ws.numel(),
             _stream(dev)), "maxk_spgemm_forward_accumulate" if accumulate else "maxk_spgemm_forward")
+    return out
+
+
+def records_ok(num_rows: int, num_cols: int, num_e: int, dim_origin: int, k: int) -> bool:
+    """Whether the forward over transport records applies (maxk_records_ok)."""
+    return bool(_lib().maxk_records_ok(int(num_rows), int(num_cols), int(num_e), int(dim_origin),
+                                       int(k)))
+
+
+def cbsr_records(cbsr_val: torch.Tensor, cbsr_idx: torch.Tensor, dim_origin: int,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Transport records [V, 5k] uint8 of a CBSR ([k f32 | k u8] per vertex; maxk_cbsr_records):
+    what a shard owner all-gathers so the receivers' forward needs no record pack."""
+    _need(cbsr_val, "cbsr_val", torch.float32)
+    _need(cbsr_idx, "cbsr_idx", torch.uint8)
+    if cbsr_val.dim() != 2 or cbsr_idx.shape != cbsr_val.shape:
+        raise RuntimeError("cbsr_val / cbsr_idx must be the same [V, k] shape")
+    V, k = cbsr_val.shape
+    if out is None:
+        out = torch.empty(V, 5 * k, dtype=torch.uint8, device=cbsr_val.device)
+    elif out.dtype != torch.uint8 or tuple(out.shape) != (V, 5 * k) or not out.is_contiguous():
+        raise RuntimeError("out must be a contiguous uint8 [V, 5k] tensor")
+    with _on(cbsr_val.device):
+        _capi.check(_lib().maxk_cbsr_records(_ptr(cbsr_val), _ptr(cbsr_idx), _ptr(out), V,
+                                             int(dim_origin), k, _stream(cbsr_val.device)),
+                    "maxk_cbsr_records")
+    return out
+
+
+def spgemm_forward_records(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
+                           rec: torch.Tensor, k: int, dim_origin: int,
+                           row_div: Optional[torch.Tensor] = None, chunk: int = 0,
+                           out: Optional[torch.Tensor] = None,
+                           accumulate: bool = False) -> torch.Tensor:
+    """spgemm_forward over transport records (cbsr_records of every column, e.g. all-gathered
+    by a sharded forward): the same sums, no record pack."""
+    _need(indptr, "indptr", torch.int32)
+    _need(indices, "indices", torch.int32)
+    _need(values, "values", torch.float32)
+    _need(rec, "rec", torch.uint8)
+    if rec.dim() != 2 or rec.shape[1] != 5 * k:
+        raise RuntimeError("rec must be [num_cols, 5k]")
+    num_rows, num_cols, E, D = indptr.numel() - 1, rec.shape[0], indices.numel(), int(dim_origin)
+    dev = rec.device
+    if row_div is not None:
+        _need(row_div, "row_div", torch.float32)
+    if out is None:
+        if accumulate:
+            raise RuntimeError("accumulate=True needs out=")
+        out = torch.empty(num_rows, D, dtype=torch.float32, device=dev)
+    L = _lib()
+    ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, num_cols, E, D, k, chunk)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    with _on(dev):
+        _capi.check(L.maxk_spgemm_forward_records(
+            _ptr(indptr), _ptr(indices), _ptr(values), _ptr(rec), _ptr(row_div), _ptr(out),
+            num_rows, num_cols, E, D, k, chunk, _ptr(ws), ws.numel(), _stream(dev),
+            1 if accumulate else 0), "maxk_spgemm_forward_records")
     return out
 
 

@@ -40,6 +40,10 @@ SIGNATURES = {
     "maxk_spgemm_forward_accumulate_sel": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64,
                                                           _i64, _i32, _i32, _i32, _p, _sz, _p,
                                                           _p]),
+    "maxk_records_ok": (ctypes.c_int, [_i64, _i64, _i64, _i32, _i32]),
+    "maxk_cbsr_records": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _i32, _p]),
+    "maxk_spgemm_forward_records": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i32,
+                                                   _i32, _i32, _p, _sz, _p, _i32]),
     "maxk_sspmm_backward_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                            _i32, _i32, _i32, _p, _sz, _p]),

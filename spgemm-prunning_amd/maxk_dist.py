@@ -33,6 +33,8 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import os
+
 import torch
 import torch.distributed as dist
 from torch.autograd import Function
@@ -349,6 +351,8 @@ class ShardedMaxK:
         # every part's two all-gathers (values, selectors: each lands as the contiguous
         # [world * vh, k] array the kernels take, no unpacking copy) queued at once, in part order
         recvs, works = [], []
+        if self._records(k, D):
+            return self._aggregate_records(sv, si, k, D, row_div_local, out)
         for j in range(P):
             rv = torch.empty(self.world * vh, k, dtype=sv.dtype, device=dev)
             ri = torch.empty(self.world * vh, k, dtype=si.dtype, device=dev)
@@ -377,6 +381,55 @@ class ShardedMaxK:
             elif col.numel() > 0:
                 self.kernels.spgemm_forward(rp, col, val, val_j, idx_j, D, row_div=row_div_local,
                                             out=y, accumulate=True, **kw)
+        return y, saved
+
+    def _records(self, k: int, D: int) -> bool:
+        """Whether the pipelined gather exchanges transport records (decided once per (k, D)):
+        the kernels offer them (cbsr_records / spgemm_forward_records), no part writes an
+        edge-selector stream, and every part with edges takes the records forward
+        (records_ok: a sparse part graph, k % 4 == 0 in [24, 32]).  MAXK_DIST_RECORDS=0: never."""
+        key = ("records", k, D)
+        if key not in self._plans:
+            kn = self.kernels
+            ok = (os.environ.get("MAXK_DIST_RECORDS", "1") != "0" and self.mode == "gather" and
+                  all(hasattr(kn, f) for f in ("cbsr_records", "spgemm_forward_records",
+                                                "records_ok")))
+            for j in range(self.pipeline):
+                rp, col, _ = self.parts[j]
+                if not ok:
+                    break
+                if col.numel() > 0:
+                    ok = (not self._stream(k, D, j) and
+                          kn.records_ok(self.n_local, self.n_cols_part, col.numel(), D, k))
+            self._plans[key] = bool(ok)
+        return self._plans[key]
+
+    def _aggregate_records(self, sv, si, k: int, D: int, row_div_local, out):
+        """The pipelined gather over transport records: each owner builds its part-j rows'
+        records ([k f32 | k u8], the bytes the two CBSR all-gathers carry), one all-gather per
+        part lands them as the [world * vh, 5k] buffer the records forward walks (no pack over
+        the gathered vertices); the part's selectors for the backward are its columns 4k..5k."""
+        P, vh = self.pipeline, self.vh
+        dev = sv.device
+        recvs, works = [], []
+        for j in range(P):
+            send = self.kernels.cbsr_records(sv[j * vh:(j + 1) * vh], si[j * vh:(j + 1) * vh], D)
+            rr = torch.empty(self.world * vh, 5 * k, dtype=torch.uint8, device=dev)
+            works.append(all_gather_rows(rr.view(-1), send.view(-1), self.group, async_op=True))
+            recvs.append(rr)
+        y, saved = out, []
+        for j in range(P):
+            _wait(works[j])
+            rr = recvs[j]
+            rp, col, val = self.parts[j]
+            saved.append((rr[:, 4 * k:].contiguous(), None))
+            if j == 0:  # writes every row (zeros where part 0 has no edges)
+                y = self.kernels.spgemm_forward_records(rp, col, val, rr, k, D,
+                                                        row_div=row_div_local, out=y)
+            elif col.numel() > 0:
+                self.kernels.spgemm_forward_records(rp, col, val, rr, k, D,
+                                                    row_div=row_div_local, out=y,
+                                                    accumulate=True)
         return y, saved
 
     def _stream(self, k: int, D: int, part: int) -> bool:

@@ -1235,3 +1235,48 @@ def test_graph_checked_once_by_default(mk, cuda, monkeypatch):
     bad_rp[-1] += 1
     with pytest.raises(RuntimeError, match="row_ptr"):
         mk.spgemm_forward(bad_rp, T(col, cuda), vl, cvt, cit, 64)
+
+
+@pytest.mark.parametrize("D,k", [(256, 32), (256, 24), (100, 28), (128, 32)])
+def test_forward_transport_records(mk, cuda, D, k):
+    """The sharded forward's transport records (maxk_cbsr_records, [k f32 | k u8] at 5k bytes)
+    walked by maxk_spgemm_forward_records: bitwise equal to maxk_spgemm_forward on the same CBSR
+    (which packs the same records itself for these shapes; before it did, the packed 256-B
+    records' walk was bitwise equal too, profiles/r05/tune/transport_records/) and against the
+    oracle, with repeated selectors and selectors >= D among clean rows, hub rows split over
+    items (chunk 40), accumulate, and zero edges; the records keep the caller's selector bytes."""
+    rng = np.random.default_rng(D * 7 + k)
+    V = 3000
+    row_ptr, col = rand_graph(rng, V, 9, hubs=((7, 900), (11, 70), (1500, 130)), empty=40)
+    val = rng.random(col.size, dtype=np.float32)
+    cv = rng.standard_normal((V, k)).astype(np.float32)
+    ci = np.stack([rng.choice(D, k, replace=False) for _ in range(V)]).astype(np.uint8)
+    dup = rng.choice(V, 60, replace=False)
+    ci[dup, -1] = ci[dup, 0]
+    if D < 256:
+        ci[rng.choice(V, 60, replace=False), 1] = rng.integers(D, 256, 60).astype(np.uint8)
+    div = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
+    args = (T(row_ptr, cuda), T(col, cuda), T(val, cuda))
+    assert mk.records_ok(V, V, col.size, D, k)
+    assert not mk.records_ok(V, V, col.size, D, 16)  # one-line records: the packed form
+    rec = mk.cbsr_records(T(cv, cuda), T(ci, cuda), D)
+    assert np.array_equal(rec.cpu().numpy()[:, 4 * k:], ci)
+    for chunk in (0, 40):
+        y = mk.spgemm_forward(*args, T(cv, cuda), T(ci, cuda), D, row_div=T(div, cuda),
+                              chunk=chunk, validate=False)
+        yr = mk.spgemm_forward_records(*args, rec, k, D, row_div=T(div, cuda), chunk=chunk)
+        assert torch.equal(y, yr)
+        acc = torch.ones(V, D, device=cuda)
+        mk.spgemm_forward_records(*args, rec, k, D, row_div=T(div, cuda), chunk=chunk, out=acc,
+                                  accumulate=True)
+        ref = torch.ones(V, D, device=cuda)
+        mk.spgemm_forward(*args, T(cv, cuda), T(ci, cuda), D, row_div=T(div, cuda), chunk=chunk,
+                          out=ref, accumulate=True, validate=False)
+        assert torch.equal(acc, ref)
+    yo = O.spgemm_fwd(row_ptr, col, val, cv, ci, 256, row_div=div)[:, :D]
+    close(yr, yo)
+    empty = (T(np.zeros(V + 1, np.int32), cuda), T(np.zeros(0, np.int32), cuda),
+             T(np.zeros(0, np.float32), cuda))
+    z = torch.full((V, D), 7.0, device=cuda)
+    mk.spgemm_forward_records(*empty, rec, k, D, out=z)
+    assert not z.any()

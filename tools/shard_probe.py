@@ -28,6 +28,9 @@ ap.add_argument("--pipelines", type=int, nargs="*", default=[],
                 help="also time the pipelined gather mode's column parts (maxk_dist PIPELINE)")
 ap.add_argument("--chunks", type=int, nargs="*", default=[],
                 help="also time rank 0's forward at these item sizes (0 = the automatic one)")
+ap.add_argument("--records", action="store_true",
+                help="forward over transport records (maxk_cbsr_records of the rank's own rows, "
+                     "timed, + maxk_spgemm_forward_records of the gathered buffer)")
 ap.add_argument("--busbw", type=float, nargs="*", default=[250.0, 375.0, 500.0],
                 help="RCCL all-gather / reduce-scatter bus bandwidths (GB/s) for the step model")
 a = ap.parse_args()
@@ -80,6 +83,21 @@ for world in a.worlds:
                             (sh.row_ptr, sh.col_idx))
         tf = timed(lambda: mk.spgemm_forward(sh.row_ptr, sh.col_idx, sh.values, cv_all, ci_all, D,
                                              out=y, validate=False))
+        if a.records and mk.records_ok(sh.n_local, sh.n_cols, sh.col_idx.numel(), D, k):
+            rec_all = mk.cbsr_records(cv_all, ci_all, D)  # what the all-gather would deliver
+            own_v, own_i = cv[sh.v0:sh.v1].contiguous(), ci[sh.v0:sh.v1].contiguous()
+            t_own = timed(lambda: mk.cbsr_records(own_v, own_i, D))
+            y2 = torch.empty_like(y)
+            t_walk = timed(lambda: mk.spgemm_forward_records(sh.row_ptr, sh.col_idx, sh.values,
+                                                             rec_all, k, D, out=y2))
+            same = bool(torch.equal(y, y2))
+            if rank == 0:
+                print(f"  N={world} rank 0 forward: packed {tf:.3f} ms, transport records "
+                      f"{t_own:.3f} (own rows) + {t_walk:.3f} (walk) = {t_own + t_walk:.3f} ms, "
+                      f"bitwise equal {same}", flush=True)
+            assert same, "transport-record forward differs from the packed one"
+            tf = t_own + t_walk
+            del rec_all, y2
         if a.chunks and rank == 0:
             line = []
             for c in a.chunks:
