@@ -161,8 +161,20 @@ if a.pipelines:
                             cij[p * vh:p * vh + hi - lo] = ci[lo:hi]
                     rp, cj, vj = sh.parts[j] if Pr > 1 else (sh.row_ptr, sh.col_idx, sh.values)
                     nc = sh.n_cols_part if Pr > 1 else sh.n_cols
-                    tf.append(timed(lambda: mk.spgemm_forward(rp, cj, vj, cvj, cij, D, out=y,
-                                                              validate=False, accumulate=j > 0)))
+                    if a.records and Pr > 1 and mk.records_ok(sh.n_local, nc, cj.numel(), D, k):
+                        # maxk_dist's transport records: the owner's part rows packed before the
+                        # all-gather (timed), the gathered part walked as it lands
+                        recj = mk.cbsr_records(cvj, cij, D)
+                        own_v = cvj[rank * vh:(rank + 1) * vh].contiguous()
+                        own_i = cij[rank * vh:(rank + 1) * vh].contiguous()
+                        t_own = timed(lambda: mk.cbsr_records(own_v, own_i, D))
+                        tf.append(t_own + timed(lambda: mk.spgemm_forward_records(
+                            rp, cj, vj, recj, k, D, out=y, accumulate=j > 0)))
+                        del recj
+                    else:
+                        tf.append(timed(lambda: mk.spgemm_forward(rp, cj, vj, cvj, cij, D, out=y,
+                                                                  validate=False,
+                                                                  accumulate=j > 0)))
                     plan = sh.plan(k, D, j if Pr > 1 else None)
                     mode = mk._bwd_mode(None, k, cj.numel(), nc, sh.n_local, D, (rp, cj))
                     gs = torch.empty(nc, k, device=dev)
