@@ -38,6 +38,10 @@ constexpr int kBucketAccDoubles = 18432;
 #ifndef MAXK_FWD_RECORDS  // streaming forward, k in [24, 32]: 5k-byte transport records instead
 #define MAXK_FWD_RECORDS 1  // of the packed ones (maxk_records_ok); 0 = the packed records
 #endif
+#ifndef MAXK_FWD_RECORDS_DEEP  // ... and in the dense graphs' deep-batch walk (Reddit k = 32
+                               // forward 3.296 -> 3.274 ms, profiles/r05/tune/transport_records/)
+#define MAXK_FWD_RECORDS_DEEP 1
+#endif
 #ifndef MAXK_FWD_WAVES
 #define MAXK_FWD_WAVES 1
 #endif

@@ -743,7 +743,7 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
         return RecordSrc{wave_buffer(trec, 0xffffffffu), 4u * lc, 4u * (uint32_t)k + lc,
                          5u * (uint32_t)k};
     };
-    const bool tr = STREAM && trec != nullptr;
+    const bool tr = (STREAM || MAXK_FWD_RECORDS_DEEP) && !WIDE && !EMIT && trec != nullptr;
 
     const int64_t total = (int64_t)num_rows + num_e;
     const int64_t d0 = (int64_t)item * chunk;
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(kBlock, EMIT ? MAXK_FWD_EMIT_WAVES : MAXK_FWD_WAVES
             rb = row_ptr[r];
             if (rb + r >= d1) break;
         }
-        if constexpr (BATCH) {
+        if (BATCH && !tr) {
             // Short-row batch: up to NC consecutive rows, each wholly inside the item and at
             // most MAXK_FWD_SHORT edges long, one per lane group, so a wave keeps NC rows'
             // loads in flight instead of walking one short row at a time (Flickr: avg
@@ -976,7 +976,8 @@ void launch_fwd(const FwdLayout &L, hipStream_t s, const int32_t *row_ptr, const
         // ms at k = 8; profiles/r04/tune/fwd_batch_depth_ab*.txt)
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, 2 * U, false, false>), grid, dim3(kBlock), lds,
                            s, row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
-                           num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, nullptr);
+                           num_rows, num_e, D, L.DS, k, L.chunk, L.n_items, accumulate, nullptr,
+                           trec);
     else if (num_cols < (1 << 24) && L.rec_bytes < (1ull << 32))
         hipLaunchKernelGGL((spgemm_fwd_kernel<KG, U, false, false>), grid, dim3(kBlock), lds, s,
                            row_ptr, col_idx, edge_val, rec, L.RS, row_div, out, slab, slab_row,
@@ -1012,7 +1013,8 @@ namespace {
 // over l, records past one line in the packed form (6k > 128, where a 5k-byte stride costs no
 // extra line per gather: 160 B at k = 32 spans two lines as the 256-B record does)
 bool records_ok(const FwdLayout &L, int64_t num_cols, int k) {
-    return L.stream && k % 4 == 0 && 6 * k > 128 && k <= L.kg && k <= 32 &&
+    return (L.stream || (MAXK_FWD_RECORDS_DEEP && L.deep)) && k % 4 == 0 && 6 * k > 128 &&
+           k <= L.kg && k <= 32 &&
            (uint64_t)num_cols * 5u * (uint64_t)k < (1ull << 32);
 }
 
