@@ -111,8 +111,8 @@ int maxk_spgemm_forward_accumulate_sel(const int32_t *row_ptr, const int32_t *co
  * selector's first occurrence carries the sum of its values in l order and the later ones, like
  * selectors >= dim_origin, a skip marker (a NaN payload; a kept NaN value is stored as the
  * canonical quiet NaN) -- the same sums as maxk_spgemm_forward.  maxk_records_ok says whether
- * the records forward applies: the streaming walker of a sparse graph (average degree < 128),
- * dim_k % 4 == 0 in [24, 32], num_cols * 5 * dim_k < 2^32 (where the 5k-byte stride costs no
+ * the records forward applies: the streaming walker of a sparse graph (average degree < 128) or
+ * the deep-batch walker of a dense one, dim_k % 4 == 0 in [24, 32], num_cols * 5 * dim_k < 2^32 (where the 5k-byte stride costs no
  * extra line per gather against the packed record).  rec 4-B aligned; workspace as
  * maxk_spgemm_forward_workspace_size; accumulate adds onto out.  Replaces the same reference
  * kernel as maxk_spgemm_forward (spmm_maxk.cu:17-113). */

@@ -1009,7 +1009,8 @@ extern "C" size_t maxk_spgemm_forward_workspace_size(int64_t num_rows, int64_t n
 }
 
 namespace {
-// the forward over transport records applies (maxk_records_ok): the streaming walker, one pass
+// the forward over transport records applies (maxk_records_ok): the streaming or (dense graphs,
+// MAXK_FWD_RECORDS_DEEP) the deep-batch walker, one pass
 // over l, records past one line in the packed form (6k > 128, where a 5k-byte stride costs no
 // extra line per gather: 160 B at k = 32 spans two lines as the 256-B record does)
 bool records_ok(const FwdLayout &L, int64_t num_cols, int k) {
