@@ -733,6 +733,9 @@ def main():
         extra.update({"dist_check_fwd_max_rel_err": dist_err[0],
                       "dist_check_bwd_max_rel_err": dist_err[1], "dist_backend": backend,
                       "dist_mode": shard.mode, "dist_pipeline": shard.pipeline,
+                      # the pipelined gather exchanged transport records (maxk_dist._records)
+                      "dist_records": bool(pipelined and shard._records(k, D)),
+                      "dist_world_observed": dist.get_world_size(),
                       # since r03 the fwd / bwd intervals hold the CBSR / gradient exchange
                       # (pipelined or not); r02's N > 1 part times held the kernels only
                       "exchange_in_interval": True,
@@ -812,6 +815,11 @@ def main():
                          # `traffic` is L2 -> fabric bytes (PMC FETCH_SIZE x2 + WRITE_SIZE): it
                          # counts Infinity-Cache hits too (MI355X_MICROARCH.md, HBM), so it is
                          # an L2-miss rate, not HBM traffic
+                         # FETCH_SIZE x2: validated per request size in r06 -- every product
+                         # kernel's fabric reads are 128-B requests (TCC_EA0_RDREQ_128B_sum =
+                         # 99.9-100 % of TCC_EA0_RDREQ_sum), sub-line record gathers included
+                         "fetch_correction": "x2 (FETCH_SIZE tallies 128-B requests at 64 B; "
+                                             "profiles/r06/fetch_calibration)",
                          "l2_miss_GBs": (round(traffic / (t_dom * 1e-3) / 1e9, 1)
                                          if traffic else None),
                          "l2_miss_frac_of_hbm_peak": (

@@ -477,13 +477,16 @@ int maxk_topk_cbsr(const float *x, int64_t ld_x, float *cbsr_val, uint8_t *cbsr_
 int maxk_topk_cbsr_u8(const uint8_t *x, int64_t ld_x, uint8_t *cbsr_val, uint8_t *cbsr_idx,
                       int32_t *idx32, int64_t num_rows, int32_t dim_origin, int32_t dim_k,
                       void *stream);
-/* The reference's uint8 top-k kernel as it behaves (kernels/maxk_kernel.cu:21-90, behind
- * cuda_topk_maxk / cuda_topk_maxk_float, cuda_kernel_bindings.cpp:164-238), for callers that
- * depend on its convention: rows of dim_origin == 256 bytes; the threshold from 8 bisection
- * steps on [0, 255]; the bytes strictly above it in ascending column order, 32 columns per step,
- * at most dim_k, a pick in column 32s + 31 overwritten by the next step's first pick (the
- * reference counts a step's picks without its lane 31); slots never filled are 0.  val / idx
- * uint8 [num_rows, dim_k].  Not torch.topk: maxk_topk_cbsr_u8 is the exact one. */
+/* The reference uint8 top-k's intended per-row convention (kernels/maxk_kernel.cu:23-94,
+ * behind cuda_topk_maxk / cuda_topk_maxk_float, cuda_kernel_bindings.cpp:164-238), for callers
+ * that depend on its layout: rows of dim_origin == 256 bytes; each row's threshold from 8
+ * bisection steps on [0, 255] over its own bytes; the bytes strictly above it in ascending
+ * column order, 32 columns per step, at most dim_k, a pick in column 32s + 31 overwritten by the
+ * next step's first pick (the reference counts a step's picks without its lane 31); slots never
+ * filled are 0.  val / idx uint8 [num_rows, dim_k].  NOT the CUDA kernel's as-built output: that
+ * kernel thresholds every row on its block's first row, per lane (:42, :44-48), racily, and
+ * leaves unfilled slots uninitialised; parity with it is unpinned (oracle/oracle.py
+ * topk_u8_reference_as_built models it).  Not torch.topk: maxk_topk_cbsr_u8 is the exact one. */
 int maxk_topk_u8_reference(const uint8_t *x, uint8_t *val, uint8_t *idx, int64_t num_rows,
                            int32_t dim_origin, int32_t dim_k, void *stream);
 /* Rows (over every top-k launch on the current device since the last reset) whose threshold

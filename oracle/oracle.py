@@ -165,17 +165,22 @@ def topk(x, k):
 
 
 def topk_u8_reference(x, k):
-    """The reference's uint8 top-k kernel per row, kernels/maxk_kernel.cu:21-90 (behind
-    cuda_topk_maxk, cuda_kernel_bindings.cpp:164-201), restated in numpy; rows of 256 bytes.
-    Threshold (:30-52): 8 bisection steps, count = #(bytes > mid); count < k: high = mid, else
-    low = mid; mid = (low + high) // 2.  Selection (:56-80): for each 32-column step (column
-    32 ext + lane), the bytes > mid go to slot total + (picks of lower lanes in the step) while
-    that is < k; then total += lane 31's exclusive prefix (:77-79: lane 31 adds its own `loc`,
-    which leaves its own pick out, so the next step's first pick overwrites it); stop once
-    total >= k (:58-61).  Slots never written stay 0 (torch::zeros, :175-176).  The kernel's
-    block-level write-out (:84-89) copies 16 rows x 32 bytes per block, i.e. it is right at
-    k = 32; this restates the per-row result at every k.  Parity unpinned against the CUDA
-    kernel itself (it cannot run here); the GPU test checks the HIP restatement against this."""
+    """The reference uint8 top-k's INTENDED per-row convention (kernels/maxk_kernel.cu:23-94,
+    behind cuda_topk_maxk, cuda_kernel_bindings.cpp:164-201), restated in numpy; rows of 256
+    bytes.  Threshold (:35-63): 8 bisection steps over the row's own bytes, count = #(bytes >
+    mid); count < k: high = mid, else low = mid; mid = (low + high) // 2.  Selection (:69-88):
+    for each 32-column step (column 32 ext + lane), the bytes > mid go to slot total + (picks of
+    lower lanes in the step) while that is < k; then total += lane 31's exclusive prefix
+    (:84-86: lane 31 adds its own `loc`, which leaves its own pick out, so the next step's first
+    pick overwrites it); stop once total >= k (:70-73).  Slots never written stay 0.
+
+    This is NOT the CUDA kernel as built: there every warp takes its threshold from
+    the block's FIRST row (:42 reads cache[laneid * 8 + j], no warp offset) with per-lane counts
+    and mids (:44-48 leaves the full sum on lane 0 only), warps 1..15 read that row across a
+    __syncwarp only (a data race), unfilled slots are uninitialised shared memory and the
+    write-out (:91-94) is right only at k = 32.  topk_u8_reference_as_built models the defined
+    part of that behaviour; the product keeps this convention.  Parity with the CUDA kernel is
+    unpinned (it cannot run here); the GPU test checks the HIP kernel against this function."""
     x = np.ascontiguousarray(x, dtype=np.uint8)
     V, D = x.shape
     if D != 256:
@@ -204,6 +209,59 @@ def topk_u8_reference(x, k):
                     idx[r, total + loc[lane]] = 32 * ext + lane
             total += int(loc[31])
     return val, idx
+
+
+def topk_u8_reference_as_built(x, k=32):
+    """A model of what the reference's uint8 top-k kernel (kernels/maxk_kernel.cu:23-94) computes
+    as built, launched as its main() and binding launch it (16 warps of 32 lanes per block, one
+    row per warp, dim_origin = 256), where that is defined: k = 32 (the block write-out at
+    :91-94 copies 16 rows x 32 bytes) and N % 16 == 0 (a partial last block reads past the
+    input).  Returns (val, idx, written): slots the kernel never writes hold uninitialised
+    shared memory there; here they are 0 and `written` is False.
+
+    Threshold (:35-63), per BLOCK and per LANE: lane l of every warp counts bytes 8l..8l+7 of
+    the block's first row (:42, no warp offset; warps 1..15 read it after a __syncwarp only --
+    modelled as if warp 0's load (:32) has landed, the one outcome that reads defined data)
+    against its own mid; the shfl_down chain (:44-48) gives lane l c[l] + c[l + d], or 2 c[l]
+    where l + d >= 32 (an out-of-range source returns the caller's own value), so only lane 0
+    holds the full count; each lane bisects its own low / high / mid from its own sum.
+    Selection (:69-88): column 32 ext + l of warp w's own row is picked when it exceeds lane
+    l's mid; compaction as in topk_u8_reference (lane 31's exclusive-prefix count)."""
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    N, D = x.shape
+    if D != 256 or k != 32 or N % 16:
+        raise ValueError("the as-built kernel is defined for [16 n, 256] rows and k = 32")
+    B = N // 16
+    row0 = x.reshape(B, 16, 256)[:, 0, :].astype(np.int64).reshape(B, 32, 8)
+    low = np.zeros((B, 32), np.int64)
+    high = np.full((B, 32), 255, np.int64)
+    mid = np.full((B, 32), 127, np.int64)
+    for _ in range(8):
+        c = (row0 > mid[:, :, None]).sum(-1)
+        for d in (16, 8, 4, 2, 1):  # count += __shfl_down_sync(count, d), all lanes at once
+            c = c + np.concatenate([c[:, d:], c[:, 32 - d:]], axis=1)
+        less = c < k
+        high = np.where(less, mid, high)
+        low = np.where(less, low, mid)
+        mid = (low + high) // 2
+    val = np.zeros((N, k), np.uint8)
+    idx = np.zeros((N, k), np.uint8)
+    written = np.zeros((N, k), bool)
+    for r in range(N):
+        m = mid[r // 16]
+        row = x[r].astype(np.int64)
+        total = 0
+        for ext in range(8):
+            if total >= k:
+                break
+            chunk = row[32 * ext:32 * ext + 32]
+            choose = chunk > m
+            loc = np.cumsum(choose) - choose
+            for lane in np.nonzero(choose & (total + loc < k))[0]:
+                s = total + loc[lane]
+                val[r, s], idx[r, s], written[r, s] = chunk[lane], 32 * ext + lane, True
+            total += int(loc[31])
+    return val, idx, written
 
 
 def warp4(row_ptr, warp_max_nz=64):

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -231,6 +232,39 @@ void clear_error();
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// CUs of the current device (hipDeviceAttributeMultiprocessorCount), cached per device ordinal:
+// the grid and work-item sizing of every launch scales with it.  256 (MI355X) when no device
+// answers (the CPU-only build check, the workspace-size queries of the C-ABI tests).
+inline int64_t device_cus() {
+    constexpr int kMaxDevices = 64;
+    static std::atomic<int> cache[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+        (void)hipGetLastError();
+        return 256;
+    }
+    int n = cache[dev].load(std::memory_order_relaxed);
+    if (n == 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0) {
+            (void)hipGetLastError();
+            n = 256;
+        }
+        cache[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
+
+// The current device's ordinal (0 without one): the key of per-device launch-size caches.
+inline int device_ordinal() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return dev;
+}
 
 // Lanes per edge group: next power of two >= k, capped at a wave.
 inline int lanes_per_edge(int k) {

@@ -598,8 +598,8 @@ int dense_lanes(int D) {
 
 // Resident waves of dense_rows_kernel on the whole device (the occupancy API on the kernel
 // that launches, times the CUs; MAXK_DENSE_WAVES per CU x 256 CUs when no device answers).
-// Cached per (lane group, SEL): the item size, and so the workspace size, stays the same for
-// the whole process.
+// The occupancy is cached per (device, lane group, kind): the item size, and so the workspace
+// size, stays the same for the whole process on each device.
 // kind: 0 dense_rows_kernel, 1 its selecting form, 2 pick_rows_kernel
 template <int LR>
 int rows_blocks_per_cu(int kind) {
@@ -620,12 +620,15 @@ int rows_blocks_per_cu(int kind) {
 }
 
 int64_t dense_slots(int lr, int kind) {
-    static std::atomic<int64_t> cache[8][3] = {};  // every thread computes the same value
+    // workgroups per CU, per device (a process with mixed devices sizes each from
+    // its own occupancy and CU count); every thread computes the same value
+    constexpr int kDevs = 16;
+    static std::atomic<int> cache[kDevs][8][3] = {};
     int li = 0;
     while ((1 << li) < lr) ++li;
-    int64_t c = cache[li][kind].load(std::memory_order_relaxed);
-    if (c == 0) {
-        int bpc = 0;
+    const int dev = device_ordinal();
+    int bpc = dev < kDevs ? cache[dev][li][kind].load(std::memory_order_relaxed) : 0;
+    if (bpc == 0) {
         switch (lr) {
             case 1: bpc = rows_blocks_per_cu<1>(kind); break;
             case 2: bpc = rows_blocks_per_cu<2>(kind); break;
@@ -635,15 +638,10 @@ int64_t dense_slots(int lr, int kind) {
             case 32: bpc = rows_blocks_per_cu<32>(kind); break;
             default: bpc = rows_blocks_per_cu<64>(kind); break;
         }
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 0;
-        (void)hipGetLastError();
-        c = bpc > 0 && cus > 0 ? (int64_t)bpc * kWavesPerBlock * cus : 256LL * MAXK_DENSE_WAVES;
-        cache[li][kind].store(c, std::memory_order_relaxed);
+        if (bpc <= 0) bpc = -1;  // no device answered: the fixed fallback below
+        if (dev < kDevs) cache[dev][li][kind].store(bpc, std::memory_order_relaxed);
     }
-    return c;
+    return bpc > 0 ? (int64_t)bpc * kWavesPerBlock * device_cus() : 256LL * MAXK_DENSE_WAVES;
 }
 
 // Items sized like the forward's (fwd_chunk): all resident in one round (90 % of the wave slots,

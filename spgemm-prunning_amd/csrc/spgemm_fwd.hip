@@ -885,15 +885,17 @@ int64_t fwd_long_rows(int64_t num_rows, int64_t num_e, int64_t c, int resident) 
     if (num_rows <= 0 || num_e < kFwdSparseDegree * num_rows) return c;
     const int64_t two_rows = (2 * ceil_div(num_e, num_rows) + 63) / 64 * 64;
     const int64_t want = two_rows < 1024 ? two_rows : 1024;
-    if (c >= want || (num_rows + num_e) / want < 256LL * resident) return c;
+    if (c >= want || (num_rows + num_e) / want < device_cus() * resident) return c;
     return want;
 }
 
 int fwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int resident) {
     if (chunk > 0) return chunk;
-    // ~8 waves of work per resident wave slot on 256 CUs, within [256, 2048] tokens
+    // ~8 waves of work per resident wave slot on the device's CUs (256 on MI355X), within
+    // [256, 2048] tokens
     const int64_t total = num_rows + num_e;
-    int64_t c = ceil_div(total, 256LL * 32 * 8);
+    const int64_t cus = device_cus();
+    int64_t c = ceil_div(total, cus * 32 * 8);
     if (c >= 256) return (int)fwd_long_rows(num_rows, num_e, c > 2048 ? 2048 : c, resident);
     // A smaller graph has fewer items than wave slots at 256 tokens: size the items so all of
     // them are resident in one round (90 % of the slots, for uneven block placement), since each
@@ -901,7 +903,7 @@ int fwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int resident) {
     // Flickr-sized (1.08M tokens, 7168 slots): 151 tokens would fill every slot; the forward at
     // 144 / 160 / 176 / 192 / 256 tokens takes 0.0527 / 0.049 / 0.051 / 0.053 / 0.0585 ms
     // (profiles/r04/tune/flickr_chunk_sweep.txt).
-    c = ceil_div(total * 10, 256LL * resident * 9);
+    c = ceil_div(total * 10, cus * resident * 9);
     return (int)fwd_long_rows(num_rows, num_e, c < 64 ? 64 : (c > 256 ? 256 : c), resident);
 }
 

@@ -1434,11 +1434,11 @@ __global__ __launch_bounds__(kBlock) void pull_reduce_kernel(const float *__rest
     reinterpret_cast<float4 *>(grad_cbsr + c0 * k)[i] = a;
 }
 
-// Auto item size: ~`per_slot` items per resident wave slot on 256 CUs, in [256, 2048].
+// Auto item size: ~`per_slot` items per resident wave slot on the device's CUs, in [256, 2048].
 int bwd_chunk(int64_t num_rows, int64_t num_e, int32_t chunk, int per_slot) {
     if (chunk > 0) return chunk;
     const int64_t total = num_rows + num_e;
-    int64_t c = ceil_div(total, 256LL * 32 * per_slot);
+    int64_t c = ceil_div(total, device_cus() * 32 * per_slot);
     c = c < 256 ? 256 : (c > 2048 ? 2048 : c);
     return (int)c;
 }
@@ -1766,7 +1766,8 @@ extern "C" int maxk_sspmm_backward_csc_sel(const int32_t *row_ptr, const int32_t
 // edge_sel_kernel's grid: one thread per word up to 64 workgroups per CU, then grid-stride
 extern "C" int64_t maxk_edge_selectors_blocks(int64_t n_words) {
     const int64_t b = ceil_div(n_words < 0 ? 0 : n_words, (int64_t)kBlock);
-    return b < 256 * 64 ? b : 256 * 64;
+    const int64_t cap = device_cus() * 64;
+    return b < cap ? b : cap;
 }
 
 extern "C" int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_idx,

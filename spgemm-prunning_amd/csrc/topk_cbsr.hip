@@ -644,14 +644,16 @@ int topk_launch(const T *x, int64_t ld_x, T *val, uint8_t *idx, int32_t *idx32, 
     return MAXK_OK;
 }
 
-// The reference's uint8 top-k as it behaves (kernels/maxk_kernel.cu:21-90, behind
-// cuda_topk_maxk / cuda_topk_maxk_float), one wave per row of 256 bytes (four per lane):
-//  * threshold: 8 bisection steps on [0, 255] -- count the bytes > mid (ballots); fewer than k:
+// The reference uint8 top-k's intended per-row convention (kernels/maxk_kernel.cu:23-94, behind
+// cuda_topk_maxk / cuda_topk_maxk_float), one wave per row of 256 bytes (four per lane).  Not
+// the CUDA kernel's as-built output, which thresholds every row on its block's first row per
+// lane (:42, :44-48) through a shared-memory race (oracle topk_u8_reference_as_built; unpinned):
+//  * threshold: 8 bisection steps on [0, 255] over the row's own bytes > mid (ballots); fewer than k:
 //    high = mid, else low = mid; mid = (low + high) / 2;
 //  * selection: the bytes strictly above mid in ascending column order, 32 columns per step
 //    (column 32 s + l on lane l), at most k; the step's count is the exclusive prefix of its
 //    lane 31, so a pick in column 32 s + 31 is overwritten by the next step's first pick, as in
-//    the reference; slots never filled stay 0 (its torch::zeros outputs).
+//    the reference; slots never filled stay 0.
 // The row's output is assembled in LDS (the overwrite order kept) and stored once.
 __global__ __launch_bounds__(kBlock) void topk_u8_reference_kernel(const uint8_t *__restrict__ x,
                                                                    uint8_t *__restrict__ val,

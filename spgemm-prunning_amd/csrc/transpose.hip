@@ -393,17 +393,6 @@ static int pull_parts_of(int32_t dim_k) {
     return H;
 }
 
-// CUs of the current device (one pull workgroup per CU at a time); 256 (MI355X) without one
-static int64_t device_cus() {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0) {
-        (void)hipGetLastError();
-        return 256;
-    }
-    return n;
-}
 
 // ~3.5 MiB of G rows per slice and part: a part gathers only its share of a row's columns
 // (its rank range of the sorted selectors), so an XCD's L2 holds H times the rows of G for

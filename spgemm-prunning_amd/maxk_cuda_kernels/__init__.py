@@ -314,23 +314,38 @@ def spgemm_forward_records(indptr: torch.Tensor, indices: torch.Tensor, values: 
                            rec: torch.Tensor, k: int, dim_origin: int,
                            row_div: Optional[torch.Tensor] = None, chunk: int = 0,
                            out: Optional[torch.Tensor] = None,
-                           accumulate: bool = False) -> torch.Tensor:
+                           accumulate: bool = False,
+                           validate: Optional[bool] = None) -> torch.Tensor:
     """spgemm_forward over transport records (cbsr_records of every column, e.g. all-gathered
-    by a sharded forward): the same sums, no record pack."""
+    by a sharded forward): the same sums, no record pack.  The same input checks as
+    spgemm_forward: dtypes, contiguity, shapes of out / row_div / values, and the
+    graph's range check (once per graph by default, every call with validate=True)."""
     _need(indptr, "indptr", torch.int32)
     _need(indices, "indices", torch.int32)
     _need(values, "values", torch.float32)
     _need(rec, "rec", torch.uint8)
-    if rec.dim() != 2 or rec.shape[1] != 5 * k:
+    k = int(k)
+    if k <= 0 or rec.dim() != 2 or rec.shape[1] != 5 * k:
         raise RuntimeError("rec must be [num_cols, 5k]")
+    if values.numel() != indices.numel():
+        raise RuntimeError("values and indices must have the same length")
     num_rows, num_cols, E, D = indptr.numel() - 1, rec.shape[0], indices.numel(), int(dim_origin)
     dev = rec.device
     if row_div is not None:
         _need(row_div, "row_div", torch.float32)
+        if row_div.numel() != num_rows:
+            raise RuntimeError("row_div must have num_rows entries")
+    # the selectors are the records' last k bytes: a strided view, read only by the selector
+    # range check (validate=True); the graph check is what bounds the kernel's record reads
+    _validate_call(validate, indptr, indices, num_cols, rec[:, 4 * k:], D)
     if out is None:
         if accumulate:
             raise RuntimeError("accumulate=True needs out=")
         out = torch.empty(num_rows, D, dtype=torch.float32, device=dev)
+    else:
+        _need(out, "out", torch.float32)
+        if tuple(out.shape) != (num_rows, D):
+            raise RuntimeError("out must be [num_rows, dim_origin]")
     L = _lib()
     ws_bytes = L.maxk_spgemm_forward_workspace_size(num_rows, num_cols, E, D, k, chunk)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
@@ -527,8 +542,11 @@ def pull_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor,
     shift = int(L.maxk_pull_shift(int(k))) if shift is None else int(shift)
     if shift < 0:
         raise RuntimeError(f"pull_plan: invalid k {k}")
-    S = int(slices) if slices else int(L.maxk_pull_slices(num_rows, int(num_cols), int(dim),
-                                                              int(k)))
+    if slices:
+        S = int(slices)
+    else:  # sized by the CU count of the device that holds the graph
+        with _on(indices.device):
+            S = int(L.maxk_pull_slices(num_rows, int(num_cols), int(dim), int(k)))
     key = (id(indptr), id(indices), id(values), shift, S)
     hit = _PULL_CACHE.get(key)
     if cache and hit is not None:
@@ -1158,9 +1176,13 @@ def _check_topk_rows(dev, name):
 
 
 def topk_u8_reference(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
-    """The reference's uint8 top-k kernel as it behaves (maxk_topk_u8_reference; rows of 256
-    bytes): (values u8 [N,k], indices u8 [N,k]) -- bytes above an 8-step bisection threshold in
-    ascending column order, its lane-31 overwrite and zero-filled slots included."""
+    """The reference uint8 top-k's intended per-row convention (maxk_topk_u8_reference; rows of
+    256 bytes): (values u8 [N,k], indices u8 [N,k]) -- the row's bytes above its own 8-step
+    bisection threshold in ascending column order, the lane-31 overwrite and zero-filled slots
+    included.  Not the CUDA kernel as built, which thresholds every row on its block's first
+    row per lane, with a shared-memory race and uninitialised slots (kernels/maxk_kernel.cu:42,
+    :44-48, :91-94; oracle.topk_u8_reference_as_built models it, and it agrees with this on
+    0.2 % of uniform rows): parity with the CUDA kernel is unpinned."""
     _need(input, "input", torch.uint8)
     if input.dim() != 2 or input.shape[1] != 256:
         raise RuntimeError("the reference's uint8 top-k takes [N, 256] rows")
@@ -1178,8 +1200,9 @@ def topk_u8_reference(input: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.
 def cuda_topk_maxk(input: torch.Tensor, k: int,
                    reference_compat: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """uint8 top-k (cuda_kernel_bindings.cpp:164-201): (values u8 [N,k], indices u8 [N,k]).
-    Exact torch.topk order by default; reference_compat=True reproduces the reference kernel's
-    own convention (topk_u8_reference: threshold bisection, ascending columns, rows of 256)."""
+    Exact torch.topk order by default; reference_compat=True takes the reference kernel's
+    intended convention (topk_u8_reference: per-row threshold bisection, ascending columns,
+    rows of 256) -- not its as-built output, which is racy; parity with it unpinned."""
     if input.dtype != torch.uint8:
         raise RuntimeError("Input must be uint8 tensor")
     if reference_compat:
@@ -1191,8 +1214,9 @@ def cuda_topk_maxk_float(input: torch.Tensor, k: int,
                          reference_compat: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """(values, int32 indices) (cuda_kernel_bindings.cpp:203-238), exact (no uint8 quantisation)
     by default.  reference_compat=True follows the reference binding: float input quantised to
-    clamp(round(x * 255), 0, 255) as uint8, the reference kernel's top-k on that
-    (topk_u8_reference), values returned as float / 255; uint8 input passes through."""
+    clamp(round(x * 255), 0, 255) as uint8, the reference kernel's intended top-k convention on
+    that (topk_u8_reference; parity with the as-built CUDA kernel unpinned), values returned as
+    float / 255; uint8 input passes through."""
     if not reference_compat:
         val, _, idx32 = topk_cbsr(input, k, with_int32=True)
         return val, idx32

@@ -123,6 +123,18 @@ class _HipKernels:
         return self.mk.sspmm_backward(indptr, indices, values, grad, cbsr_idx, row_div=row_div,
                                       plan=plan, mode=self.bwd_mode, edge_sel=edge_sel)
 
+    # the transport-record forward (ShardedMaxK._records / _aggregate_records)
+    def records_ok(self, num_rows, num_cols, num_e, dim, k):
+        return self.mk.records_ok(num_rows, num_cols, num_e, dim, k)
+
+    def cbsr_records(self, cbsr_val, cbsr_idx, dim):
+        return self.mk.cbsr_records(cbsr_val, cbsr_idx, dim)
+
+    def spgemm_forward_records(self, indptr, indices, values, rec, k, D, row_div=None, out=None,
+                               accumulate=False):
+        return self.mk.spgemm_forward_records(indptr, indices, values, rec, k, D,
+                                              row_div=row_div, out=out, accumulate=accumulate)
+
     def stream_mode(self, indptr, indices, k, num_cols, num_rows=None, dim=None):
         """Whether a (part's) forward should write the edge-selector stream for its backward:
         the backward this graph resolves to reads one ("csc" / "bsort") and

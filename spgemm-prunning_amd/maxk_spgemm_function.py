@@ -67,9 +67,17 @@ def _converted(src, tag, make):
     so an int64 indptr, a warp4 array or float64 values converted afresh every step would
     rebuild them (and re-synchronise the host) on every call.  Graph-side tensors
     only (indices, indptr, edge values, warp4, degrees): activations are converted uncached
-    (_f32_act), so no fp32 copy of a [V, D] input outlives its call.  Inference
-    tensors carry no version counter and are converted uncached too."""
-    if src.is_inference() or torch.is_inference_mode_enabled():
+    (_f32_act), so no fp32 copy of a [V, D] input outlives its call.
+
+    Under torch.inference_mode (an evaluation pass over a graph loaded outside it) the
+    conversion is made with inference mode off: a normal tensor, versioned, so this cache and
+    the plan / graph-check caches keyed on it hit on every later call.  An
+    inference tensor itself (a graph built inside inference mode) has no version counter and
+    can still change in place there: it is converted afresh on every call, and the caches
+    downstream of it miss -- one conversion, one host-synchronising graph check and, for the
+    pull / csc backward, one plan build per call; build the graph outside inference mode to
+    avoid that."""
+    if src.is_inference():
         return make(src)
     key = (id(src), tag)
     hit = _CONVERTED.get(key)
@@ -77,7 +85,11 @@ def _converted(src, tag, make):
         ref, ver, out = hit
         if ref() is src and ver == src._version:
             return out
-    out = make(src)
+    if torch.is_inference_mode_enabled():
+        with torch.inference_mode(False):
+            out = make(src)
+    else:
+        out = make(src)
     if out is src:  # nothing converted: the caller's own tensor, no cache entry needed
         return out
     if key not in _CONVERTED:

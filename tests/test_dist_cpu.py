@@ -50,6 +50,27 @@ class OracleKernels:
         return torch.from_numpy(g)
 
 
+class OracleRecordKernels(OracleKernels):
+    """OracleKernels plus the transport-record surface (records_ok / cbsr_records /
+    spgemm_forward_records), so the CPU tests take ShardedMaxK's record route: records are the
+    [k f32 | k u8] bytes of each CBSR row, unpacked for the oracle's forward."""
+
+    def records_ok(self, num_rows, num_cols, num_e, dim, k):
+        return k % 4 == 0 and 24 <= k <= 32
+
+    def cbsr_records(self, cbsr_val, cbsr_idx, dim):
+        k = cbsr_val.shape[1]
+        return torch.cat([cbsr_val.contiguous().view(torch.uint8).view(-1, 4 * k),
+                          cbsr_idx.contiguous()], 1).contiguous()
+
+    def spgemm_forward_records(self, indptr, indices, values, rec, k, D, row_div=None, out=None,
+                               accumulate=False):
+        cv = rec[:, :4 * k].contiguous().view(torch.float32)
+        ci = rec[:, 4 * k:].contiguous()
+        return self.spgemm_forward(indptr, indices, values, cv, ci, D, row_div=row_div, out=out,
+                                   accumulate=accumulate)
+
+
 def make_graph(V, avg_deg, seed, hub=True):
     rng = np.random.default_rng(seed)
     deg = rng.poisson(avg_deg, V).astype(np.int64)
@@ -72,7 +93,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gather",
-            pipeline=1):
+            pipeline=1, records=False):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -87,8 +108,11 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gat
 
         shard = maxk_dist.ShardedMaxK(torch.from_numpy(row_ptr), torch.from_numpy(col),
                                       torch.from_numpy(val), rank, world,
-                                      kernels=OracleKernels(), bounds=bounds, mode=mode,
+                                      kernels=OracleRecordKernels() if records
+                                      else OracleKernels(), bounds=bounds, mode=mode,
                                       pipeline=pipeline)
+        if records:  # the record route is what runs (every part's forward over records)
+            assert shard.pipeline > 1 and shard._records(k, D)
         v0, v1 = shard.v0, shard.v1
         div = torch.from_numpy(deg[v0:v1]) if use_div else None
         val_l = torch.from_numpy(tv[v0:v1]).requires_grad_(True)
@@ -104,13 +128,13 @@ def _worker(rank, world, port, V, D, k, seed, use_div, q, bounds=None, mode="gat
 
 
 def _run(world, V=400, D=64, k=8, seed=0, use_div=True, bounds=None, mode="gather",
-         pipeline=1):
+         pipeline=1, records=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
                          args=(r, world, port, V, D, k, seed, use_div, q, bounds, mode,
-                               pipeline))
+                               pipeline, records))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -175,6 +199,31 @@ def test_sharded_matches_single_process_world8(mode, pipeline):
         np.testing.assert_allclose(gs, gs_ref[v0:v1], rtol=1e-5, atol=BWD_ATOL)
         covered += v1 - v0
     assert covered == V
+
+
+@pytest.mark.parametrize("world,pipeline,bounds", [(2, 2, None), (4, 3, None),
+                                                   (3, 2, [0, 150, 150, 400])])
+def test_sharded_transport_records(world, pipeline, bounds):
+    """The pipelined gather over transport records (ShardedMaxK._aggregate_records: each owner
+    packs its part rows as [k f32 | k u8] records, one uint8 all-gather per part, the records
+    forward per part; the backward reads the parts' selectors out of the records) against the
+    single-process oracle, k = 32; the last case has an empty rank."""
+    V, D, k, seed = 400, 64, 32, 5
+    outs = _run(world, V, D, k, seed, True, bounds, "gather", pipeline, records=True)
+    y_ref, gs_ref = _single(V, D, k, seed, True)
+    covered = 0
+    for rank, v0, v1, y, gs, bounds_, xb, n_cols in outs:
+        np.testing.assert_allclose(y, y_ref[v0:v1], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(gs, gs_ref[v0:v1], rtol=1e-5, atol=BWD_ATOL)
+        covered += v1 - v0
+    assert covered == V
+
+
+def test_hip_backend_offers_records():
+    """The HIP backend exposes the record surface ShardedMaxK._records looks for (r05 left it
+    off _HipKernels, so the record route never ran outside the CPU stand-in)."""
+    for f in ("records_ok", "cbsr_records", "spgemm_forward_records"):
+        assert callable(getattr(maxk_dist._HipKernels, f))
 
 
 def test_balanced_bounds_properties():
@@ -290,26 +339,43 @@ def test_sharded_hip_single_rank_rccl(cuda):
     os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
     try:
-        V, D, k = 3000, 256, 16
+        V, D = 3000, 256
         row_ptr, col, val = make_graph(V, 9, 5)
         rng = np.random.default_rng(2)
         x = rng.standard_normal((V, D)).astype(np.float32)
         g = rng.standard_normal((V, D)).astype(np.float32)
         deg = np.maximum(np.diff(row_ptr), 1).astype(np.float32)
-        tv, ti = oracle.topk(x, k)
         to = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
-        y_ref = oracle.spgemm_fwd(row_ptr, col, val, tv, ti, D, row_div=deg)
-        gs_ref = oracle.sspmm_bwd(row_ptr, col, val, g, ti, row_div=deg)
-        for pipeline in (None, 3):
+        refs = {}
+        # (k, pipeline, mode): the plain and pipelined gathers at k = 16 (two async RCCL
+        # all-gathers per part); k = 32 pipelined through the transport records (VERDICT r05
+        # item 1: cbsr_records + one uint8 async all-gather per part, the records forward, the
+        # parts' reduce-scatters); the halo exchange (all_to_all_single on RCCL, the plan's two
+        # all-to-alls and the forward / backward ones) at k = 16 and 32
+        for k, pipeline, mode in ((16, None, "gather"), (16, 3, "gather"), (32, 2, "gather"),
+                                  (16, None, "halo"), (32, None, "halo")):
+            if k not in refs:
+                tv, ti = oracle.topk(x, k)
+                refs[k] = (tv, ti, oracle.spgemm_fwd(row_ptr, col, val, tv, ti, D, row_div=deg),
+                           oracle.sspmm_bwd(row_ptr, col, val, g, ti, row_div=deg))
+            tv, ti, y_ref, gs_ref = refs[k]
             shard = maxk_dist.ShardedMaxK(to(row_ptr), to(col), to(val), 0, 1, device=cuda,
-                                          pipeline=pipeline)
-            assert shard.pipeline == (1 if pipeline is None else 3)
-            val_l = to(tv).requires_grad_(True)
-            y = maxk_dist.sharded_maxk_spgemm(shard, val_l, to(ti), D, to(deg))
-            y.backward(to(g))
-            np.testing.assert_allclose(y.detach().cpu().numpy(), y_ref, rtol=1e-4, atol=1e-4)
-            np.testing.assert_allclose(val_l.grad.cpu().numpy(), gs_ref, rtol=1e-4, atol=1e-4)
-            if pipeline is None:
+                                          pipeline=pipeline, mode=mode, k=k)
+            assert shard.mode == mode
+            assert shard.pipeline == (1 if pipeline is None else pipeline)
+            if pipeline is not None:
+                assert shard._records(k, D) == (k == 32), (k, pipeline)
+            if mode == "halo":
+                assert shard.n_cols == np.unique(col).size and shard.send_counts == [shard.n_cols]
+            for _ in range(2):  # the second step reuses the plans and the cached graph check
+                val_l = to(tv).requires_grad_(True)
+                y = maxk_dist.sharded_maxk_spgemm(shard, val_l, to(ti), D, to(deg))
+                y.backward(to(g))
+                torch.cuda.synchronize()
+                np.testing.assert_allclose(y.detach().cpu().numpy(), y_ref, rtol=1e-4, atol=1e-4)
+                np.testing.assert_allclose(val_l.grad.cpu().numpy(), gs_ref, rtol=1e-4,
+                                           atol=1e-4)
+            if pipeline is None and mode == "gather":
                 y2 = mk.spgemm_forward(to(row_ptr), to(col), to(val), to(tv), to(ti), D,
                                        row_div=to(deg))
                 assert torch.equal(y.detach(), y2)

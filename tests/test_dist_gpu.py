@@ -142,30 +142,38 @@ def test_sharded_forced_backward_modes(graph, single, bwd, stream, monkeypatch):
     _run_world(graph, single, 2, "gloo")
 
 
-def test_bench_self_launch_products_world2():
-    """BASELINE.json configs[3] at its real size through the driver's own command shape
-    (VERDICT r04 item 1): `python bench.py --gpus 2 ...` with no WORLD_SIZE starts its two
-    ranks itself (bench.launch_ranks: a child torch.distributed.run, gloo-staged collectives
-    on this one GPU), shards the ogbn-products-sized graph (V = 2,449,029, E = 123.7M, k = 32)
-    by vertex range and checks every rank's forward rows and CBSR-gradient rows against the
-    unsharded HIP result, which tests/test_fullsize_gpu.py pins to the oracle on every row."""
+@pytest.mark.parametrize("graph,k,gpus,records", [("products", 32, 2, True),
+                                                  ("products", 32, 4, True),
+                                                  ("reddit", 16, 8, False)])
+def test_bench_self_launch(graph, k, gpus, records):
+    """BASELINE.json configs[3] (and the driver's default-graph SCALE shape) at real size through
+    the driver's own command shape: `python bench.py --gpus N
+    ...` with no WORLD_SIZE starts its N ranks itself (bench.launch_ranks: a child
+    torch.distributed.run, gloo-staged collectives on this one GPU), shards the graph by vertex
+    range and checks every rank's forward rows and CBSR-gradient rows against the unsharded HIP
+    result, which tests/test_fullsize_gpu.py pins to the oracle on every row.  ogbn-products at
+    k = 32 (V = 2,449,029, E = 123.7M) takes the pipelined transport-record exchange at N = 2 and
+    4; Reddit at k = 16 and N = 8 (`bench.py --gpus 8`, the driver's default graph) one part.
+    World > 1 over RCCL itself stays unmeasured on this one-GPU box."""
     import json
     env = dict(os.environ)
     env.pop("WORLD_SIZE", None)
     env["MAXK_DIST_BACKEND"] = "gloo"
     env.pop("MAXK_VALIDATE", None)  # the bench validates its graph once itself
     root = os.path.dirname(HERE)
-    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
-                        "--graph", "products", "--k", "32", "--steps", "2", "--warmup", "1"],
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", str(gpus),
+                        "--graph", graph, "--k", str(k), "--steps", "2", "--warmup", "1"],
                        env=env, cwd=root, capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
     e = d["extra"]
-    assert d["n_gpus"] == 2 and d["config"]["V"] == 2449029 and d["config"]["k"] == 32
-    assert d["config"]["parallelism"] == "vertex-range x2"
-    assert e["dist_backend"] == "gloo"
+    V = {"products": 2449029, "reddit": 232965}[graph]
+    assert d["n_gpus"] == gpus and d["config"]["V"] == V and d["config"]["k"] == k
+    assert d["config"]["parallelism"] == f"vertex-range x{gpus}"
+    assert e["dist_backend"] == "gloo" and e["dist_world_observed"] == gpus
+    assert e["dist_records"] == records, e
     assert e["dist_check_fwd_max_rel_err"] <= 1e-5, e
     assert e["dist_check_bwd_max_rel_err"] <= 1e-5, e
     assert e["adjoint_rel_err"] <= 1e-6, e

@@ -126,3 +126,30 @@ def test_topk_u8_reference_restatement():
     v, i = O.topk_u8_reference(x, 4)
     assert v[0].tolist() == [200, 180, 220, 0] and i[0].tolist() == [3, 40, 63, 0]
     assert i[1].tolist() == [0, 1, 2, 3] and v[1].tolist() == [255, 254, 253, 252]
+
+
+def test_topk_u8_as_built_model():
+    """The CUDA kernel as built (oracle.topk_u8_reference_as_built): every warp
+    takes its threshold from the block's first row, per lane.  By hand: a block whose first row
+    is all zero bisects every lane's mid down to 0, so row 1 (255 .. 0) picks every nonzero byte
+    in column order -- columns 0..30, then column 32 over lane 31's uncounted pick -- while its
+    own threshold (the intended convention) would pick its 32 largest; row 0 picks nothing.
+    On uniform bytes the two conventions disagree on most rows, which is why the product keeps
+    the intended one (reference_compat) and calls parity with the CUDA kernel unpinned."""
+    x = np.zeros((16, 256), np.uint8)
+    x[1] = np.arange(256)[::-1]
+    x[2:] = np.random.default_rng(0).integers(0, 256, (14, 256), dtype=np.uint8)
+    v, i, w = O.topk_u8_reference_as_built(x, 32)
+    assert not w[0].any()
+    assert i[1].tolist() == list(range(31)) + [32] and w[1].all()
+    assert v[1].tolist() == list(range(255, 224, -1)) + [223]
+    vi, ii = O.topk_u8_reference(x, 32)
+    assert ii[1].tolist() != i[1].tolist()
+    with pytest.raises(ValueError):
+        O.topk_u8_reference_as_built(x, 16)
+    u = np.random.default_rng(1).integers(0, 256, (256, 256), dtype=np.uint8)
+    va, ia, wa = O.topk_u8_reference_as_built(u, 32)
+    vi, ii = O.topk_u8_reference(u, 32)
+    differ = np.mean([not (np.array_equal(ia[r][wa[r]], ii[r][:wa[r].sum()]) and wa[r].all())
+                      for r in range(256)])
+    assert differ > 0.5, differ

@@ -556,6 +556,15 @@ def test_autograd_v1_inference_mode_bf16(F, cuda):
     assert len(Fm._CONVERTED) == n0  # nothing cached: inference tensors, activations
     y32 = F.maxk_spgemm(col, val, xb.float(), int(z["k"]), graph_indptr=ip, in_degrees=deg)
     assert torch.equal(y, y32.detach()) and torch.equal(y_nc, y32.detach())
+    # an int64 graph loaded outside inference mode and evaluated inside it is
+    # converted once (a normal, versioned int32 copy), so every later call hits the caches
+    ip64 = ip.long()
+    with torch.inference_mode():
+        ys = [F.maxk_spgemm(col, val, xb, int(z["k"]), graph_indptr=ip64, in_degrees=deg)
+              for _ in range(2)]
+    hit = Fm._CONVERTED[(id(ip64), "i32")]
+    assert len(Fm._CONVERTED) == n0 + 1 and not hit[2].is_inference()
+    assert torch.equal(ys[0], y32.detach()) and torch.equal(ys[1], y32.detach())
 
 
 @pytest.mark.parametrize("path", CASES, ids=IDS)
@@ -1264,11 +1273,12 @@ def test_forward_transport_records(mk, cuda, D, k):
     for chunk in (0, 40):
         y = mk.spgemm_forward(*args, T(cv, cuda), T(ci, cuda), D, row_div=T(div, cuda),
                               chunk=chunk, validate=False)
-        yr = mk.spgemm_forward_records(*args, rec, k, D, row_div=T(div, cuda), chunk=chunk)
+        yr = mk.spgemm_forward_records(*args, rec, k, D, row_div=T(div, cuda), chunk=chunk,
+                                       validate=False)
         assert torch.equal(y, yr)
         acc = torch.ones(V, D, device=cuda)
         mk.spgemm_forward_records(*args, rec, k, D, row_div=T(div, cuda), chunk=chunk, out=acc,
-                                  accumulate=True)
+                                  accumulate=True, validate=False)
         ref = torch.ones(V, D, device=cuda)
         mk.spgemm_forward(*args, T(cv, cuda), T(ci, cuda), D, row_div=T(div, cuda), chunk=chunk,
                           out=ref, accumulate=True, validate=False)
@@ -1277,6 +1287,21 @@ def test_forward_transport_records(mk, cuda, D, k):
     close(yr, yo)
     empty = (T(np.zeros(V + 1, np.int32), cuda), T(np.zeros(0, np.int32), cuda),
              T(np.zeros(0, np.float32), cuda))
+    # the input checks spgemm_forward makes: graph ranges, out / row_div shapes
+    if D < 256:
+        with pytest.raises(RuntimeError, match="sparse_selector"):
+            mk.spgemm_forward_records(*args, rec, k, D, validate=True)
+    bad = args[1].clone()
+    bad[5] = V
+    with pytest.raises(RuntimeError, match="col_idx out of range"):
+        mk.spgemm_forward_records(args[0], bad, args[2], rec, k, D, validate=True)
+    with pytest.raises(RuntimeError, match="out must be"):
+        mk.spgemm_forward_records(*args, rec, k, D, out=torch.empty(V, D + 1, device=cuda),
+                                  validate=False)
+    with pytest.raises(RuntimeError, match="row_div"):
+        mk.spgemm_forward_records(*args, rec, k, D, row_div=T(div[:-1], cuda), validate=False)
+    with pytest.raises(RuntimeError, match="same length"):
+        mk.spgemm_forward_records(args[0], args[1], args[2][:-1], rec, k, D, validate=False)
     z = torch.full((V, D), 7.0, device=cuda)
     mk.spgemm_forward_records(*empty, rec, k, D, out=z)
     assert not z.any()
