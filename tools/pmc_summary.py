@@ -2,7 +2,10 @@
 """Summarise rocprofv3 --pmc counter CSVs per kernel (mean per dispatch).
 
 FETCH_SIZE/WRITE_SIZE are KB; on gfx950 FETCH_SIZE reads 1/2 of wide streaming
-bytes (MI355X_MICROARCH.md, HBM) -- the corrected column doubles it.
+bytes (MI355X_MICROARCH.md, HBM) -- the corrected column doubles it.  r06 validated the
+doubling for every product kernel, sub-line gathers included: their fabric reads are all
+128-B requests (TCC_EA0_RDREQ_128B_sum / TCC_EA0_RDREQ_sum >= 0.999), tallied at 64 B each
+(tools/fetch_probe.hip, profiles/r06/fetch_calibration/).
 
   pmc_summary.py CSV... [--traffic-out profiles/rNN/traffic.json --key WORKLOAD]
 

@@ -33,6 +33,10 @@
 #             box: the bench line (3 repeats) and the 3-layer epoch (2 repeats)
 #   kt        the reference's kernel test (maxk_kernel_test.py) on every config graph, k = 8..64
 #   epochs    3-layer MaxK-SAGE epochs against the rocSPARSE model
+#   fetchcal  tools/fetch_probe (known 64/80/128/160/256-B record gathers and a streaming read,
+#             24 MiB and 2 GiB tables) under a FETCH_SIZE pass and a fabric-request-size pass
+#             (TCC_EA0_RDREQ_sum / _32B / _128B), summarised by tools/fetch_probe_summary.py
+#             (r06: the FETCH_SIZE correction per request size)
 #   collect   (here, not on the box) copy gpurun_out/<round> into profiles/<round> and write
 #             the summaries (kernel stats, PMC traffic.json, presets and kernel-test tables)
 set -eo pipefail
@@ -158,6 +162,18 @@ set_one() {
 step_pmcset() {
   mkdir -p $O/pmc_set
   cfg_loop set_one
+}
+step_fetchcal() {
+  mkdir -p $O/fetch
+  timeout -k 10 120 tools/fetch_probe > $O/fetch/probe.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/fetch/p1 -o run --output-format csv \
+    -- tools/fetch_probe > $O/fetch/p1.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum \
+    TCC_EA0_RDREQ_128B_sum -d $O/fetch/p2 -o run --output-format csv \
+    -- tools/fetch_probe > $O/fetch/p2.log 2>&1
+  python3 tools/fetch_probe_summary.py $O/fetch/probe.log $(find $O/fetch -name '*counter_collection.csv') \
+    > $O/fetch/summary.txt
+  cat $O/fetch/summary.txt
 }
 step_statscfg() {
   mkdir -p $O/stats_cfg
