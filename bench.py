@@ -413,7 +413,7 @@ def main():
     ap.add_argument("--no-rocsparse", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--bwd-mode", default="auto",
-                    choices=["auto", "pull", "bucket", "csc", "atomic", "hybrid", "bsort", "dense"])
+                    choices=["auto", "pull", "csc", "atomic", "hybrid", "bsort", "dense"])
     ap.add_argument("--graph-dir", default=None,
                     help="use <dir>/<graph>.indptr|.indices (the reference's files) when present")
     ap.add_argument("--no-cpu-spmm", action="store_true")

@@ -193,42 +193,14 @@ int maxk_transpose_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
                         int32_t *col_ptr, int32_t *csc_eid, void *workspace,
                         size_t workspace_bytes, void *stream);
 
-/* ---------------------------------------------------------------------------
- * Same backward, two-phase with a bucketed phase 2 (k % 4 == 0):
- * phase 1 as in maxk_sspmm_backward_csc; phase 2 gives every bucket of 2^bucket_shift
- * consecutive destinations one workgroup, which reads the bucket's contribution rows in
- * CSR order (neighbouring rows share cache lines) and sums them in an fp64 LDS
- * accumulator.  The fp32 result does not depend on the order of the adds except in rare
- * rounding ties (fp64 partial sums); use maxk_sspmm_backward_csc where every bit must
- * repeat.  Needs dim_k % 4 == 0 and 2^bucket_shift * (dim_k + 1) <= 18432, the bucket plan of
- * the graph built with that shift (maxk_bucket_plan) and a workspace of
- * maxk_sspmm_backward_bucket_workspace_size(...) bytes (about num_e*k*4).
- * Replaces the same reference kernels as maxk_sspmm_backward.
- * ------------------------------------------------------------------------- */
-size_t maxk_sspmm_backward_bucket_workspace_size(int64_t num_rows, int64_t num_cols,
-                                                 int64_t num_e, int32_t dim_origin,
-                                                 int32_t dim_k, int32_t chunk_edges);
-int maxk_sspmm_backward_bucket(const int32_t *row_ptr, const int32_t *col_idx,
-                               const float *edge_val, const float *grad_out, const float *row_div,
-                               const uint8_t *cbsr_idx, const int32_t *bucket_ptr,
-                               const int32_t *bucket_eid, const uint16_t *bucket_dst,
-                               int32_t bucket_shift, float *grad_cbsr, int64_t num_rows,
-                               int64_t num_cols, int64_t num_e, int32_t dim_origin, int32_t dim_k,
-                               int32_t chunk_edges, void *workspace, size_t workspace_bytes,
-                               void *stream);
-
-/* Bucket plan of a CSR graph (once per graph and shift): bucket_ptr[nb+1] with
- * nb = maxk_bucket_count(num_cols, shift), bucket_eid[num_e] = the CSR edge ids whose
- * column lies in each bucket (in CSR order), bucket_dst[num_e] = that column minus the
- * bucket's first column.  maxk_bucket_shift(k) is the largest shift the accumulator
- * allows for k (-1 for k <= 0).  Like maxk_transpose_plan, the MI355X replacement for the
- * CSC side files of generate_meta_csc.py:14-93 / load_warp4_metadata_csc. */
+/* Destination buckets (the pull's tiles, the bsort plan, the hybrid plan): buckets of
+ * 2^bucket_shift consecutive columns, nb = maxk_bucket_count(num_cols, shift) of them;
+ * maxk_bucket_shift(k) is the largest shift the fp64 LDS accumulator of the bucketed phase 2
+ * allows for k (-1 for k <= 0).  (r06: the "bucket" backward mode and its plan entry points,
+ * which no BASELINE configuration reached, left the library; bsort keeps the bucketed
+ * phase 2.) */
 int maxk_bucket_shift(int32_t dim_k);
 int64_t maxk_bucket_count(int64_t num_cols, int32_t bucket_shift);
-size_t maxk_bucket_plan_workspace_size(int64_t num_cols, int64_t num_e);
-int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
-                     int32_t bucket_shift, int32_t *bucket_ptr, int32_t *bucket_eid,
-                     uint16_t *bucket_dst, void *workspace, size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Same backward, two-phase with window-sorted contribution rows ("bsort", dim_k % 4 == 0),
@@ -236,13 +208,13 @@ int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
  * otherwise cost a whole random 128-B line (ogbn-products k = 8: 32-B rows).  The CSR edges
  * are cut into windows of W = maxk_bsort_window(dim_k) consecutive edges; phase 1 builds a
  * window's rows in LDS (one workgroup per window) and writes them to the window's range of T
- * ordered by destination bucket, so the bucketed phase 2 (as maxk_sspmm_backward_bucket,
- * fp64 LDS sums) reads a bucket's rows of one window as one run.  edge_sel (optional, u8
+ * ordered by destination bucket, so the bucketed phase 2 (one workgroup per part of a
+ * bucket's entry list, fp64 LDS sums) reads a bucket's rows of one window as one run.  edge_sel (optional, u8
  * [num_e, k], 4-B aligned; as maxk_sspmm_backward_csc_sel) replaces the cbsr_idx row
  * gathers; cbsr_idx may be NULL when it is given, col_idx when edge_sel is given.
  * Plan (once per graph and k): maxk_bsort_plan with the shift maxk_bucket_shift(k) --
- * bucket_ptr / bucket_dst as maxk_bucket_plan, bucket_pos[num_e] the T row of each bucket
- * entry, win_src[num_e] (u16) the edge (relative to its window) whose row T row p holds,
+ * bucket_ptr[nb + 1] the start of each bucket's entries, bucket_dst[num_e] (u16) each entry's
+ * column minus its bucket's first column, bucket_pos[num_e] the T row of each bucket entry, win_src[num_e] (u16) the edge (relative to its window) whose row T row p holds,
  * edge_row[num_e] the source row of every CSR edge.
  * Meant for dim_k <= MAXK_BSORT_KMAX (8; the auto rule's limit): W * 4 * dim_k bytes fill the LDS
  * stage, so larger k leaves fewer rows per window and bucket (k = 16 on ogbn-products: one
@@ -394,7 +366,7 @@ int maxk_sspmm_backward_dense(const int32_t *col_ptr, const int32_t *t_src, cons
  *   dim_origin / 4 <= dim_k < dim_origin / 2, both % 4 == 0; else MAXK_BWD_PULL where
  *   dim_k % 4 == 0 or dim_k <= 64, dim_origin % 4 == 0 and the graph has at
  *   least ~1/2 edge per (source row, bucket of 2^maxk_bucket_shift(dim_k) columns) or a G of at
- *   most 64 MiB; else MAXK_BWD_BUCKET on such a dense graph at dim_k <= 16; else MAXK_BWD_HYBRID
+ *   most 64 MiB (and at most 256 x 65536 rows); else MAXK_BWD_HYBRID
  *   when pull_locality (maxk_pull_locality at maxk_pull_shift(dim_k); < 0 = unknown) reaches
  *   MAXK_HYBRID_LOCALITY and dim_k % 4 == 0; else MAXK_BWD_BSORT at dim_k % 4 == 0,
  *   dim_k <= MAXK_BSORT_KMAX when a window of maxk_bsort_window(dim_k) edges holds at least 2
@@ -421,7 +393,7 @@ int maxk_sspmm_backward_dense(const int32_t *col_ptr, const int32_t *t_src, cons
  * ------------------------------------------------------------------------- */
 #define MAXK_BWD_PULL 0
 #define MAXK_BWD_CSC 1
-#define MAXK_BWD_BUCKET 2
+/* 2 was MAXK_BWD_BUCKET (removed in r06); the code stays unused */
 #define MAXK_BWD_HYBRID 3
 #define MAXK_BWD_ATOMIC 4
 #define MAXK_BWD_BSORT 5

@@ -387,7 +387,6 @@ extern "C" int maxk_backward_mode_auto(int64_t num_rows, int64_t num_cols, int64
         dim_origin % 4 == 0 && dense_pick(dim_origin, k))
         return MAXK_BWD_DENSE;
     if ((dense || small) && rows <= 256LL * 65536) return MAXK_BWD_PULL;
-    if (dense && k <= 16 && k % 4 == 0) return MAXK_BWD_BUCKET;
     if (k % 4 == 0 && rows <= 256LL * 65536 && num_e > 0 && pull_locality >= MAXK_HYBRID_LOCALITY)
         return MAXK_BWD_HYBRID;
     // window-sorted contribution rows where a window holds runs of >= 2 rows per bucket

@@ -17,9 +17,10 @@
 //  * two-phase: phase 1 (the push) stores each edge's contribution row in CSR edge order
 //    (non-temporal 16-B buffer stores, so the 7.3 GB stream does not evict the
 //    selector table every edge gathers from), then
-//    - bucket (maxk_sspmm_backward_bucket): per bucket of destinations, the rows are read
-//      in CSR order (neighbouring rows share lines) and summed in an fp64 LDS accumulator
-//      (bucket_sum_kernel below);
+//    - bsort (maxk_sspmm_backward_bsort): phase 1 writes each window of CSR edges' rows
+//      ordered by destination bucket; per bucket of destinations the rows are read as runs
+//      and summed in an fp64 LDS accumulator (bucket_sum_kernel below; the plain "bucket"
+//      mode over CSR-ordered rows left the library in r06);
 //    - csc (maxk_sspmm_backward_csc): per destination, the rows are gathered through the
 //      CSC permutation and summed in a fixed order; bitwise deterministic.
 // Phase 1 and the csc phase 2 use the token-stream work partition of common.h (one wave
@@ -1790,7 +1791,7 @@ extern "C" int maxk_edge_selectors(const int32_t *col_idx, const uint8_t *cbsr_i
 
 // Bucketed phase 2: entries per part (~MAXK_BUCKET_PARTS parts per CU, at least 16384).
 int bucket_part(int64_t num_e) {
-    int64_t p = ceil_div(num_e, 256LL * MAXK_BUCKET_PARTS);
+    int64_t p = ceil_div(num_e, device_cus() * MAXK_BUCKET_PARTS);
     return (int)(p < 16384 ? 16384 : p);
 }
 
@@ -1799,10 +1800,9 @@ static int bucket_phase2(hipStream_t s, const float *T, const int32_t *bucket_pt
                          float *grad_cbsr, void *workspace, int64_t num_cols, int64_t num_e,
                          int k);
 
-extern "C" size_t maxk_sspmm_backward_bucket_workspace_size(int64_t num_rows, int64_t num_cols,
-                                                            int64_t num_e, int32_t dim_origin,
-                                                            int32_t dim_k, int32_t chunk_edges) {
-    (void)num_rows; (void)num_cols; (void)dim_origin; (void)chunk_edges;
+// Workspace of the bucketed phase 2 (bsort): T [E + 1, k] floats, then 2 slab rows of
+// 2^shift * k floats per part (the parts' first and last buckets)
+static size_t bucket_workspace_size(int64_t num_e, int32_t dim_k) {
     if (num_e < 0 || dim_k <= 0) return 0;
     const int shift = maxk_bucket_shift(dim_k);
     const size_t t = ((size_t)(num_e + 1) * dim_k * sizeof(float) + 255) & ~(size_t)255;
@@ -1810,48 +1810,9 @@ extern "C" size_t maxk_sspmm_backward_bucket_workspace_size(int64_t num_rows, in
     return t + parts * 2 * ((size_t)dim_k << shift) * sizeof(float);
 }
 
-extern "C" int maxk_sspmm_backward_bucket(const int32_t *row_ptr, const int32_t *col_idx,
-                                          const float *edge_val, const float *grad_out,
-                                          const float *row_div, const uint8_t *cbsr_idx,
-                                          const int32_t *bucket_ptr, const int32_t *bucket_eid,
-                                          const uint16_t *bucket_dst, int32_t bucket_shift,
-                                          float *grad_cbsr, int64_t num_rows, int64_t num_cols,
-                                          int64_t num_e, int32_t dim_origin, int32_t dim_k,
-                                          int32_t chunk_edges, void *workspace,
-                                          size_t workspace_bytes, void *stream) {
-    clear_error();
-    if (int rc = check_common(num_rows, num_cols, num_e, dim_origin, dim_k, chunk_edges)) return rc;
-    MAXK_REQUIRE(dim_k % 4 == 0, "bucketed backward needs dim_k %% 4 == 0, got %d", dim_k);
-    MAXK_REQUIRE(bucket_shift >= 0 && bucket_shift <= 16 &&
-                     ((int64_t)(dim_k + 1) << bucket_shift) <= kBucketAccDoubles,
-                 "bucket_shift %d too large for dim_k %d (2^shift * (k + 1) <= %d)", bucket_shift,
-                 dim_k, kBucketAccDoubles);
-    hipStream_t s = as_stream(stream);
-    if (num_cols == 0) return MAXK_OK;
-    MAXK_REQUIRE(grad_cbsr && bucket_ptr, "grad_cbsr/bucket_ptr must not be NULL");
-    MAXK_REQUIRE(num_e == 0 || (row_ptr && col_idx && edge_val && grad_out && cbsr_idx &&
-                                bucket_eid && bucket_dst),
-                 "CSR/grad/selector/bucket pointers must not be NULL");
-    const size_t need = maxk_sspmm_backward_bucket_workspace_size(num_rows, num_cols, num_e,
-                                                                  dim_origin, dim_k, chunk_edges);
-    MAXK_REQUIRE(workspace && workspace_bytes >= need,
-                 "workspace too small: need %zu bytes, got %zu", need, workspace_bytes);
-    float *T = reinterpret_cast<float *>(workspace);
-    const int k = dim_k;
-    if (num_e > 0 && num_rows > 0) {
-        if (int rc = launch_push<kStore>(s, row_ptr, col_idx, edge_val, grad_out, row_div,
-                                         cbsr_idx, T, (int)num_rows, num_cols, num_e,
-                                         dim_origin, k,
-                                         bwd_chunk(num_rows, num_e, chunk_edges, MAXK_P1_ITEMS)))
-            return rc;
-    }
-    return bucket_phase2(s, T, bucket_ptr, bucket_eid, bucket_dst, bucket_shift, grad_cbsr,
-                         workspace, num_cols, num_e, k);
-}
-
 // Phase 2 of the bucketed forms: bucket_sum_kernel over the bucket list (entry i reads T row
 // bucket_row[i]) and the fixup of the buckets split over parts.  The slab sits after T in
-// the workspace (maxk_sspmm_backward_bucket_workspace_size).
+// the workspace (bucket_workspace_size).
 static int bucket_phase2(hipStream_t s, const float *T, const int32_t *bucket_ptr,
                          const int32_t *bucket_row, const uint16_t *bucket_dst, int bucket_shift,
                          float *grad_cbsr, void *workspace, int64_t num_cols, int64_t num_e,
@@ -1902,8 +1863,8 @@ extern "C" int32_t maxk_bsort_window(int32_t dim_k) {
 extern "C" size_t maxk_sspmm_backward_bsort_workspace_size(int64_t num_rows, int64_t num_cols,
                                                            int64_t num_e, int32_t dim_origin,
                                                            int32_t dim_k) {
-    return maxk_sspmm_backward_bucket_workspace_size(num_rows, num_cols, num_e, dim_origin, dim_k,
-                                                     0);
+    (void)num_rows; (void)num_cols; (void)dim_origin;
+    return bucket_workspace_size(num_e, dim_k);
 }
 
 extern "C" int maxk_sspmm_backward_bsort(

@@ -126,15 +126,17 @@ extern "C" int64_t maxk_bucket_count(int64_t num_cols, int32_t bucket_shift) {
     return (num_cols + (1LL << bucket_shift) - 1) >> bucket_shift;
 }
 
-extern "C" size_t maxk_bucket_plan_workspace_size(int64_t num_cols, int64_t num_e) {
+// The bucket plan (internal since r06: only the window-sorted bsort plan builds one; the
+// "bucket" backward mode it served is gone).
+static size_t bucket_plan_workspace_size(int64_t num_cols, int64_t num_e) {
     if (num_cols < 0 || num_e <= 0) return 0;
     return 2 * al256((size_t)num_e * 4) + al256(sort_temp_bytes(num_e, num_cols));
 }
 
-extern "C" int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
-                                int32_t bucket_shift, int32_t *bucket_ptr, int32_t *bucket_eid,
-                                uint16_t *bucket_dst, void *workspace, size_t workspace_bytes,
-                                void *stream) {
+static int bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_t num_e,
+                       int32_t bucket_shift, int32_t *bucket_ptr, int32_t *bucket_eid,
+                       uint16_t *bucket_dst, void *workspace, size_t workspace_bytes,
+                       void *stream) {
     clear_error();
     MAXK_REQUIRE(num_cols >= 0 && num_cols < (1LL << 31), "num_cols out of range");
     MAXK_REQUIRE(num_e >= 0 && num_e < (1LL << 31), "num_e out of range");
@@ -147,7 +149,7 @@ extern "C" int maxk_bucket_plan(const int32_t *col_idx, int64_t num_cols, int64_
         return MAXK_OK;
     }
     MAXK_REQUIRE(col_idx && bucket_eid && bucket_dst, "col_idx/bucket_eid/bucket_dst must not be NULL");
-    const size_t need = maxk_bucket_plan_workspace_size(num_cols, num_e);
+    const size_t need = bucket_plan_workspace_size(num_cols, num_e);
     MAXK_REQUIRE(workspace && workspace_bytes >= need, "workspace too small: need %zu", need);
     char *ws = reinterpret_cast<char *>(workspace);
     const size_t a = al256((size_t)num_e * 4);
@@ -235,7 +237,7 @@ size_t bsort_sort_bytes(int64_t num_e) {
 extern "C" size_t maxk_bsort_plan_workspace_size(int64_t num_cols, int64_t num_e) {
     if (num_cols < 0 || num_e <= 0) return 0;
     const size_t a = al256((size_t)num_e * 4);
-    const size_t bucket = maxk_bucket_plan_workspace_size(num_cols, num_e);
+    const size_t bucket = bucket_plan_workspace_size(num_cols, num_e);
     const size_t own = 4 * a + al256(bsort_sort_bytes(num_e));
     return own > bucket ? own : bucket;
 }
@@ -258,7 +260,7 @@ extern "C" int maxk_bsort_plan(const int32_t *row_ptr, const int32_t *col_idx, i
                  "%lld windows x %lld buckets exceed the 31-bit sort key", (long long)nwin,
                  (long long)nb);
     // the bucket plan, its edge ids landing in bucket_pos (num_e == 0: bucket_ptr zeroed)
-    if (int rc = maxk_bucket_plan(col_idx, num_cols, num_e, bucket_shift, bucket_ptr, bucket_pos,
+    if (int rc = bucket_plan(col_idx, num_cols, num_e, bucket_shift, bucket_ptr, bucket_pos,
                                   bucket_dst, workspace, workspace_bytes, stream))
         return rc;
     if (num_e == 0) return MAXK_OK;

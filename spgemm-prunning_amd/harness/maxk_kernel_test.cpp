@@ -153,7 +153,6 @@ const char *mode_name(int m) {
     switch (m) {
         case MAXK_BWD_PULL: return "pull";
         case MAXK_BWD_CSC: return "csc";
-        case MAXK_BWD_BUCKET: return "bucket";
         case MAXK_BWD_HYBRID: return "hybrid";
         case MAXK_BWD_ATOMIC: return "atomic";
         case MAXK_BWD_BSORT: return "bsort";
@@ -165,7 +164,6 @@ const char *mode_name(int m) {
 int mode_of(const std::string &s) {
     if (s == "pull") return MAXK_BWD_PULL;
     if (s == "csc") return MAXK_BWD_CSC;
-    if (s == "bucket") return MAXK_BWD_BUCKET;
     if (s == "hybrid") return MAXK_BWD_HYBRID;
     if (s == "atomic") return MAXK_BWD_ATOMIC;
     if (s == "bsort") return MAXK_BWD_BSORT;
@@ -256,26 +254,6 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
                     b.off_ip.as<int32_t>(), b.off_col.as<int32_t>(), b.off_val.as<float>(),
                     b.counts[2], b.off_cp.as<int32_t>(), b.off_eid.as<int32_t>(), 0, out, V, V, D,
                     k, b.ws.p, b.ws.n, nullptr, nullptr, nullptr, nullptr));
-            };
-            return;
-        }
-        case MAXK_BWD_BUCKET: {
-            b.shift = maxk_bucket_shift(k);
-            const int64_t nb = maxk_bucket_count(V, b.shift);
-            b.plan_a.alloc((size_t)(nb + 1) * 4);
-            b.plan_b.alloc((size_t)E * 4);
-            b.plan_c.alloc((size_t)E * 2);
-            Buf pws(maxk_bucket_plan_workspace_size(V, E));
-            MAXK_CHECK(maxk_bucket_plan(ci, V, E, b.shift, b.plan_a.as<int32_t>(),
-                                        b.plan_b.as<int32_t>(), b.plan_c.as<uint16_t>(), pws.p,
-                                        pws.n, nullptr));
-            HIP_CHECK(hipDeviceSynchronize());
-            b.ws.alloc(maxk_sspmm_backward_bucket_workspace_size(V, V, E, D, k, 0));
-            b.run = [&b, rp, ci, ev, G, row_div, S, out, V, E, D, k] {
-                MAXK_CHECK(maxk_sspmm_backward_bucket(rp, ci, ev, G, row_div, S,
-                                                      b.plan_a.as<int32_t>(), b.plan_b.as<int32_t>(),
-                                                      b.plan_c.as<uint16_t>(), b.shift, out, V, V,
-                                                      E, D, k, 0, b.ws.p, b.ws.n, nullptr));
             };
             return;
         }

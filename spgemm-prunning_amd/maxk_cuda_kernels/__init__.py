@@ -46,7 +46,7 @@ __all__ = [
     "topk_cbsr", "cbsr_scatter_dense", "topk_cbsr_dense", "topk_backward", "topk_error_rows",
     "build_warp4_metadata", "warp4_to_indptr",
     "spgemm_forward", "sspmm_backward", "DenseSpMMPlan", "version", "device_count",
-    "transpose_plan", "bucket_plan", "bsort_plan", "pull_plan", "edge_selector_mode", "backward_plan", "BWD_MODES",
+    "transpose_plan", "bsort_plan", "pull_plan", "edge_selector_mode", "backward_plan", "BWD_MODES",
 ]
 
 FULL_DIM = 256  # the reference binding's fixed output width (cuda_kernel_bindings.cpp:70)
@@ -428,46 +428,6 @@ def dense_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor
     return plan
 
 
-_BUCKET_CACHE: "dict" = {}
-
-
-def bucket_plan(indices: torch.Tensor, num_cols: int, k: int, cache: bool = True):
-    """(bucket_ptr int32 [nb+1], bucket_eid int32 [E], bucket_dst uint16 [E], shift) of the
-    CSR column indices for the bucketed backward at width k: per bucket of 2^shift
-    destinations, the CSR edge ids whose column lies in it (CSR order) and that column
-    relative to the bucket.  Built once per graph and shift on the GPU (stable radix sort on
-    the column bits >= shift); cached per `indices` tensor object (and its version counter)."""
-    _need(indices, "indices", torch.int32)
-    L = _lib()
-    shift = int(L.maxk_bucket_shift(int(k)))
-    if shift < 0:
-        raise RuntimeError(f"bucket_plan: invalid k {k}")
-    key = (id(indices), shift)
-    hit = _BUCKET_CACHE.get(key)
-    if cache and hit is not None:
-        ref, nc, ver, plan = hit
-        if ref() is indices and nc == num_cols and ver == _ver(indices):
-            return plan
-    dev = indices.device
-    E = indices.numel()
-    nb = int(L.maxk_bucket_count(num_cols, shift))
-    bptr = torch.empty(nb + 1, dtype=torch.int32, device=dev)
-    beid = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
-    bdst = torch.empty(max(E, 1), dtype=torch.uint16, device=dev)[:E]
-    ws = torch.empty(max(1, L.maxk_bucket_plan_workspace_size(num_cols, E)), dtype=torch.uint8,
-                     device=dev)
-    with _on(dev):
-        _capi.check(L.maxk_bucket_plan(_ptr(indices), num_cols, E, shift, _ptr(bptr), _ptr(beid),
-                                       _ptr(bdst), _ptr(ws), ws.numel(), _stream(dev)),
-                    "maxk_bucket_plan")
-    plan = (bptr, beid, bdst, shift)
-    if cache:
-        if key not in _BUCKET_CACHE:
-            weakref.finalize(indices, _BUCKET_CACHE.pop, key, None)
-        _BUCKET_CACHE[key] = (weakref.ref(indices), int(num_cols), _ver(indices), plan)
-    return plan
-
-
 _BSORT_CACHE: "dict" = {}
 
 
@@ -581,8 +541,7 @@ _HYBRID_CACHE: "dict" = {}
 MAXK_PULL_NO_REDUCE, MAXK_PULL_REDUCE_ONLY = 2, 4  # include/maxk_hip.h
 MAXK_HYBRID_PRESCALED = 1
 # maxk_backward_mode_auto's codes (include/maxk_hip.h MAXK_BWD_*)
-_MODE_OF_CODE = {0: "pull", 1: "csc", 2: "bucket", 3: "hybrid", 4: "atomic", 5: "bsort",
-                 6: "dense"}
+_MODE_OF_CODE = {0: "pull", 1: "csc", 3: "hybrid", 4: "atomic", 5: "bsort", 6: "dense"}
 _SIDE: "dict" = {}
 
 
@@ -666,7 +625,7 @@ def hybrid_plan(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tenso
     return plan
 
 
-BWD_MODES = ("auto", "pull", "bucket", "csc", "atomic", "hybrid", "bsort", "dense")
+BWD_MODES = ("auto", "pull", "csc", "atomic", "hybrid", "bsort", "dense")
 BSORT_KMAX = 8  # MAXK_BSORT_KMAX: the auto rule's bsort limit
 _BSORT_WARNED: set = set()  # (id(indptr), k) already warned about
 
@@ -758,15 +717,16 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
     or k <= 64, dim % 4 == 0 when dim is given, and at least ~1/2 edge per (source row,
     bucket of 2^maxk_bucket_shift(k) columns) on average (Reddit k=16: 2.2, k=64: 0.54;
     ogbn-proteins k=64: 1.2; ogbn-products: 0.02), or a gradient G of at most 64 MiB (Flickr:
-    23 MB, 0.05 vs 0.13 ms), which stays cache-resident however sparse the graph; for more
-    than 256 x 65536 rows "bucket" (k <= 16) stands in.  On a sparse graph the whole pull loses
+    23 MB, 0.05 vs 0.13 ms), which stays cache-resident however sparse the graph (at most
+    256 x 65536 rows; past that the rules below apply).  On a sparse graph the whole pull loses
     even with locality (its per-slice partials, [num_cols, k] per row slice: a community-
     ordered ogbn-products-sized graph 46 ms against 8 ms csc), but where
     `graph` = (indptr, indices) is given and its pull_locality reaches HYBRID_LOCALITY (k % 4
     == 0, dim % 4 == 0) "hybrid" pulls the dense tiles and runs csc over the rest (that graph:
     4.7 against 7.4 ms); otherwise "bsort" at k % 4 == 0, k <= 8 when a window of
     maxk_bsort_window(k) edges holds >= 2 rows per destination bucket on average (ogbn-
-    products k = 8: 2.9 against 3.9 ms for csc, both with the selector stream), else "csc".  "pull", "bucket" and "hybrid" sum in fp64 LDS accumulators: two runs
+    products k = 8: 2.9 against 3.9 ms for csc, both with the selector stream), else "csc".
+    "pull", "bsort" and "hybrid" sum in fp64 LDS accumulators: two runs
     agree except in rare fp32 rounding ties; MAXK_BWD_MODE=csc forces the bitwise-
     deterministic form everywhere."""
     mode = mode or os.environ.get("MAXK_BWD_MODE", "auto")
@@ -782,7 +742,7 @@ def _bwd_mode(mode: Optional[str], k: int = 4, num_e: int = 0, num_cols: int = 0
             loc = pull_locality(graph[0], graph[1], int(L.maxk_pull_shift(int(k))))
             code = int(L.maxk_backward_mode_auto(rows, num_cols, num_e, D, int(k), loc))
         mode = _MODE_OF_CODE[code]
-    if mode in ("bucket", "bsort") and k % 4 != 0:
+    if mode == "bsort" and k % 4 != 0:
         raise RuntimeError(f"backward mode '{mode}' needs k % 4 == 0, got k={k}")
     if mode == "pull" and k % 4 != 0 and k > 64:
         raise RuntimeError(f"backward mode 'pull' needs k % 4 == 0 or k <= 64, got k={k}")
@@ -815,8 +775,6 @@ def backward_plan(indices: torch.Tensor, num_cols: int, k: int, mode: Optional[s
         if indptr is None or values is None:
             raise RuntimeError("backward_plan: mode 'dense' needs indptr= and values=")
         return dense_plan(indptr, indices, values, num_cols)
-    if mode == "bucket":
-        return bucket_plan(indices, num_cols, k)
     if mode == "bsort":
         if indptr is None:
             raise RuntimeError("backward_plan: mode 'bsort' needs indptr=")
@@ -845,14 +803,12 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
     uses the graph's pull plan (built once per (indptr, indices, values) and cached, or
     `plan=` from pull_plan()); fp64 tile sums, so two runs agree except in rare rounding
     ties (use "csc" for bitwise repeatability).
-    mode "bucket": two-phase with a bucketed phase 2 summing in fp64 LDS accumulators, using
-    the graph's bucket plan (built once and cached, or `plan=` from bucket_plan()).
     mode "csc": two-phase, atomic-free and bitwise deterministic, using the graph's
     transpose plan (built once and cached, or `plan=` from transpose_plan()).
-    mode "bsort" (k % 4 == 0): two-phase like "bucket", phase 1 writing each window of
-    maxk_bsort_window(k) CSR edges' rows ordered by destination bucket (staged in LDS), so
-    phase 2 reads a bucket's rows of a window as one run -- for large sparse graphs at small
-    k, where a csc or bucket phase 2 pays a whole random line per 32-B row (bsort_plan()).
+    mode "bsort" (k % 4 == 0): two-phase, phase 1 writing each window of maxk_bsort_window(k)
+    CSR edges' rows ordered by destination bucket (staged in LDS), phase 2 summing each
+    bucket's rows of a window as one run in fp64 LDS accumulators -- for large sparse graphs
+    at small k, where a csc phase 2 pays a whole random line per 32-B row (bsort_plan()).
     mode "atomic": one global fp32 atomic per (edge, l); no preprocessing.
     mode "dense" (k % 4 == 0, dim % 4 == 0; "auto" picks it at k >= dim / 2, dim <= 128,
     maxk_dense_route): Y = A^T diag(1/row_div) G over dense G rows along the graph's transpose
@@ -967,17 +923,6 @@ def sspmm_backward(indptr: torch.Tensor, indices: torch.Tensor, values: torch.Te
                 _ptr(grad_output), _ptr(row_div), _ptr(cbsr_idx), _ptr(tptr), _ptr(ent), shift,
                 S, _ptr(out), num_rows, num_cols, E, D, k, _ptr(ws), ws.numel(), _stream(dev)),
                 "maxk_sspmm_backward_pull")
-        return out
-    if mode == "bucket":
-        bptr, beid, bdst, shift = plan if plan is not None else bucket_plan(indices, num_cols, k)
-        ws_bytes = L.maxk_sspmm_backward_bucket_workspace_size(num_rows, num_cols, E, D, k, chunk)
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        with _on(dev):
-            _capi.check(L.maxk_sspmm_backward_bucket(
-                _ptr(indptr), _ptr(indices), _ptr(values), _ptr(grad_output), _ptr(row_div),
-                _ptr(cbsr_idx), _ptr(bptr), _ptr(beid), _ptr(bdst), shift, _ptr(out), num_rows,
-                num_cols, E, D, k, chunk, _ptr(ws), ws.numel(), _stream(dev)),
-                "maxk_sspmm_backward_bucket")
         return out
     if mode == "bsort":
         if k > BSORT_KMAX and (id(indptr), k) not in _BSORT_WARNED:

@@ -61,14 +61,8 @@ SIGNATURES = {
     "maxk_sspmm_backward_dense_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
     "maxk_sspmm_backward_dense": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64,
                                                  _i32, _i32, _i32, _p, _sz, _p]),
-    "maxk_sspmm_backward_bucket_workspace_size": (_sz, [_i64, _i64, _i64, _i32, _i32, _i32]),
-    "maxk_sspmm_backward_bucket": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p,
-                                                  _i64, _i64, _i64, _i32, _i32, _i32, _p, _sz,
-                                                  _p]),
     "maxk_bucket_shift": (ctypes.c_int, [_i32]),
     "maxk_bucket_count": (_i64, [_i64, _i32]),
-    "maxk_bucket_plan_workspace_size": (_sz, [_i64, _i64]),
-    "maxk_bucket_plan": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _p, _p, _sz, _p]),
     "maxk_bsort_window": (_i32, [_i32]),
     "maxk_bsort_plan_workspace_size": (_sz, [_i64, _i64]),
     "maxk_bsort_plan": (ctypes.c_int, [_p, _p, _i64, _i64, _i64, _i32, _i32, _p, _p, _p, _p, _p,

@@ -109,7 +109,7 @@ def main(argv=None):
     ap.add_argument("--graph-dir", default=None)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--runs", type=int, default=20)
-    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "pull", "bucket", "bsort", "csc", "atomic", "dense"])
+    ap.add_argument("--bwd-mode", default="auto", choices=["auto", "pull", "bsort", "csc", "atomic", "dense"])
     ap.add_argument("--json", action="store_true", help="also print one JSON summary line")
     args = ap.parse_args(argv)
     if not torch.cuda.is_available():

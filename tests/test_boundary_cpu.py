@@ -155,8 +155,9 @@ def test_autograd_surface_no_cpu_fallback():
 
 def test_backward_mode_resolution():
     """mode "auto": pull for k % 4 == 0 or k <= 64, dim % 4 == 0 and >= 1/2 edge per (source
-    row, bucket) or a small G, else csc; "bucket" refuses k % 4 != 0, "pull" k % 4 != 0 above
-    64 and dim % 4 != 0; unknown modes are rejected (no silent fallback)."""
+    row, bucket) or a small G, else csc; "bsort" refuses k % 4 != 0, "pull" k % 4 != 0 above
+    64 and dim % 4 != 0; unknown modes are rejected (no silent fallback), "bucket" (removed in
+    r06) among them; a dense graph past the pull's 256 x 65536 rows goes to csc."""
     import maxk_cuda_kernels as mk
     reddit = dict(num_e=114_615_891, num_cols=232_965, num_rows=232_965)
     products = dict(num_e=123_718_280, num_cols=2_449_029, num_rows=2_449_029)
@@ -210,11 +211,12 @@ def test_backward_mode_resolution():
         mk._bwd_mode("bsort", 6, **reddit)
     # a shard of 1/8 of the rows keeps Reddit's per-row degree: still the pull form
     assert mk._bwd_mode("auto", 16, num_e=14_326_986, num_cols=232_968, num_rows=29_121) == "pull"
-    assert mk._bwd_mode("bucket", 16, **reddit) == "bucket"
+    with pytest.raises(RuntimeError, match="backward mode must be one of"):
+        mk._bwd_mode("bucket", 16, **reddit)
+    huge = 256 * 65536 + 1  # Reddit's density past the pull's row limit: csc
+    assert L.maxk_backward_mode_auto(huge, huge, 492 * huge, 256, 16, -1.0) == 1
     assert mk._bwd_mode("csc", 16, **reddit) == "csc"
     assert mk._bwd_mode("atomic", 3, **reddit) == "atomic"
-    with pytest.raises(RuntimeError):
-        mk._bwd_mode("bucket", 6, **reddit)
     with pytest.raises(RuntimeError):
         mk._bwd_mode("pull", 66, **reddit)
     with pytest.raises(RuntimeError):

@@ -41,12 +41,12 @@ def _write_graph(d, z):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bwd", ["auto", "pull", "csc", "hybrid", "bucket", "bsort", "atomic"])
+@pytest.mark.parametrize("bwd", ["auto", "pull", "csc", "hybrid", "bsort", "atomic"])
 @pytest.mark.parametrize("path", golden_cases()[:4], ids=lambda p: os.path.basename(p)[:-4])
 def test_harness_reproduces_golden(cuda, tmp_path, path, bwd):
     z = load_golden(path)
     k, D = int(z["k"]), int(z["D"])
-    if bwd in ("bucket", "bsort", "hybrid") and k % 4:
+    if bwd in ("bsort", "hybrid") and k % 4:
         pytest.skip("needs k % 4 == 0")
     if bwd in ("pull", "hybrid") and D % 4:
         pytest.skip("needs D % 4 == 0")

@@ -1,4 +1,4 @@
-"""Probe, not product: the window-sorted backward (mode "bsort") against csc and bucket on a
+"""Probe, not product: the window-sorted backward (mode "bsort") against csc on a
 synthetic preset graph, with and without the per-edge selector stream; checks bsort against
 csc and times each whole call (HIP events).  Run under rocprofv3 --kernel-trace --stats for
 the phase split.
@@ -55,7 +55,6 @@ for k in a.k:
     err = ((got - ref).abs() / ref.abs().clamp(min=1)).max().item()
     r = {}
     for name, mode, plan, sel in (("csc", "csc", tplan, None), ("csc+stream", "csc", tplan, es),
-                                  ("bucket", "bucket", None, None),
                                   ("bsort", "bsort", bplan, None),
                                   ("bsort+stream", "bsort", bplan, es)):
         r[name] = t(lambda: mk.sspmm_backward(row_ptr, col, val, G, ci, row_div=div, mode=mode,

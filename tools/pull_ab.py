@@ -46,8 +46,8 @@ def t(f):
     return s.elapsed_time(e) / a.iters
 
 
-ref_mode = "bucket" if k % 4 == 0 else "csc"  # the reference form the pull is checked against
-bplan = mk.bucket_plan(col, V, k) if ref_mode == "bucket" else mk.transpose_plan(col, V)
+ref_mode = "csc"  # the reference form the pull is checked against
+bplan = mk.transpose_plan(col, V)
 out = torch.empty(V, k, device=dev)
 
 

@@ -37,6 +37,10 @@
 #             24 MiB and 2 GiB tables) under a FETCH_SIZE pass and a fabric-request-size pass
 #             (TCC_EA0_RDREQ_sum / _32B / _128B), summarised by tools/fetch_probe_summary.py
 #             (r06: the FETCH_SIZE correction per request size)
+#   contention  tools/shard_probe.py at N = 8 (products k = 32, the pipelined record exchange)
+#             with each part's kernels also timed beside a paced copy standing in for the
+#             overlapping RCCL collective (tools/paced_copy.hip, 32 and 64 channels): the
+#             contention-inclusive N = 8 step model (r06)
 #   collect   (here, not on the box) copy gpurun_out/<round> into profiles/<round> and write
 #             the summaries (kernel stats, PMC traffic.json, presets and kernel-test tables)
 set -eo pipefail
@@ -95,7 +99,7 @@ step_presets() {
   mkdir -p $O/presets
   preset reddit
   for k in 8 32 64; do preset reddit_k$k --k $k; done
-  for m in bucket csc atomic; do preset reddit_$m --bwd-mode $m --no-rocsparse; done
+  for m in csc atomic; do preset reddit_$m --bwd-mode $m --no-rocsparse; done
   for k in 8 16 32 64; do preset products_k$k --graph products --k $k; done
   preset products_k4 --graph products --k 4 --no-rocsparse
   preset proteins --graph proteins
@@ -174,6 +178,16 @@ step_fetchcal() {
   python3 tools/fetch_probe_summary.py $O/fetch/probe.log $(find $O/fetch -name '*counter_collection.csv') \
     > $O/fetch/summary.txt
   cat $O/fetch/summary.txt
+}
+step_contention() {
+  mkdir -p $O/scaling
+  local ch
+  for ch in 32 64; do
+    timeout -k 10 400 python tools/shard_probe.py --graph products --k 32 --worlds 1 8 \
+      --pipelines 2 --records --contention --channels $ch \
+      > $O/scaling/contention_products_k32_ch$ch.txt 2>&1
+    tail -12 $O/scaling/contention_products_k32_ch$ch.txt
+  done
 }
 step_statscfg() {
   mkdir -p $O/stats_cfg

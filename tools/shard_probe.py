@@ -33,6 +33,12 @@ ap.add_argument("--records", action="store_true",
                      "timed, + maxk_spgemm_forward_records of the gathered buffer)")
 ap.add_argument("--busbw", type=float, nargs="*", default=[250.0, 375.0, 500.0],
                 help="RCCL all-gather / reduce-scatter bus bandwidths (GB/s) for the step model")
+ap.add_argument("--contention", action="store_true",
+                help="pipelined mode: also time each part's kernels beside a paced copy on a "
+                     "second stream that moves the overlapping collective's bytes at each --busbw "
+                     "with --channels workgroups (tools/paced_copy.hip; r06, VERDICT r05 item 4)")
+ap.add_argument("--channels", type=int, default=32,
+                help="workgroups of the collective stand-in (RCCL: one per channel)")
 a = ap.parse_args()
 P = maxk_graph.PRESETS[a.graph]
 k = a.k or P["k"]
@@ -118,6 +124,70 @@ for world in a.worlds:
           f"({worst[2]} edges, bwd {worst[4]}){eff}", flush=True)
 
 
+_PACED = None
+
+
+def paced_lib():
+    """tools/probe_lib/libpaced_copy.so (build: see tools/paced_copy.hip)."""
+    global _PACED
+    if _PACED is None:
+        import ctypes
+        _PACED = ctypes.CDLL(os.path.join(ROOT, "tools", "probe_lib", "libpaced_copy.so"))
+        _PACED.paced_copy.restype = ctypes.c_int
+        _PACED.paced_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                      ctypes.c_void_p]
+    return _PACED
+
+
+_BUF = {}
+
+
+def timed_beside(f, nbytes, reduce, gbps):
+    """(ms of f, ms of the paced copy) with f on the current stream and a paced copy of nbytes
+    (a reduce-copy reading two buffers when `reduce`) started with it on a second stream."""
+    n = max(16, nbytes // 16 * 16)
+    if _BUF.get("n", 0) < n:
+        _BUF.clear()
+        _BUF.update(n=n, src=torch.empty(n // 4, device=dev), src2=torch.empty(n // 4, device=dev),
+                    dst=torch.empty(n // 4, device=dev), side=torch.cuda.Stream())
+    side, cur = _BUF["side"], torch.cuda.current_stream()
+    lib = paced_lib()
+    tf = tc = 0.0
+    for it in range(3 + a.iters):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record(cur)
+        side.wait_event(e0)
+        rc = lib.paced_copy(_BUF["src"].data_ptr(), _BUF["src2"].data_ptr() if reduce else None,
+                            _BUF["dst"].data_ptr(), n, a.channels, gbps, side.cuda_stream)
+        assert rc == 0, rc
+        f()
+        e1.record(cur)
+        e2.record(side)
+        cur.wait_stream(side)
+        torch.cuda.synchronize()
+        if it >= 3:
+            tf += e0.elapsed_time(e1)
+            tc += e0.elapsed_time(e2)
+    return tf / a.iters, tc / a.iters
+
+
+def step_model_c(tf, tfc, tb, tbc, a_ms, ac_ms, r_ms, rc_ms):
+    """step_model with the contention measured: forward part j < P-1 runs beside all-gather j+1
+    (tfc[j]; that all-gather takes ac_ms), backward part j > 0 beside reduce-scatter j-1 (tbc[j];
+    rc_ms); the first all-gather and the last reduce-scatter run alone (a_ms, r_ms)."""
+    P = len(tf)
+    t_ag = t_f = 0.0
+    for j in range(P):
+        t_ag += ac_ms if j > 0 else a_ms
+        t_f = max(t_f, t_ag) + (tfc[j] if j < P - 1 else tf[j])
+    t_b = t_rs = 0.0
+    for j in range(P):
+        t_b += tbc[j] if j > 0 else tb[j]
+        t_rs = max(t_rs, t_b) + (rc_ms if j < P - 1 else r_ms)
+    return t_f + max(t_b, t_rs)
+
+
 def step_model(parts_f, parts_b, ag_bytes, rs_bytes, world, busbw):
     """Step time (ms) of one rank: the forward's all-gathers queued back to back on the
     communicator's stream, part j's product after its all-gather (j > 0 accumulating); the
@@ -150,7 +220,7 @@ if a.pipelines:
                 b, vh, Pr = sh.bounds, (sh.vh if sh.pipeline > 1 else sh.vmax), sh.pipeline
                 gl = G[sh.v0:sh.v1].contiguous()
                 y = torch.empty(sh.n_local, D, device=dev)
-                tf, tb = [], []
+                tf, tb, cont = [], [], {}
                 for j in range(Pr):
                     cvj = torch.zeros(world * vh, k, device=dev)
                     cij = torch.zeros(world * vh, k, dtype=torch.uint8, device=dev)
@@ -178,15 +248,40 @@ if a.pipelines:
                     plan = sh.plan(k, D, j if Pr > 1 else None)
                     mode = mk._bwd_mode(None, k, cj.numel(), nc, sh.n_local, D, (rp, cj))
                     gs = torch.empty(nc, k, device=dev)
-                    tb.append(timed(lambda: mk.sspmm_backward(rp, cj, vj, gl, cij, out=gs,
-                                                              validate=False, mode=mode,
-                                                              plan=plan)))
+                    def bwd_j():
+                        mk.sspmm_backward(rp, cj, vj, gl, cij, out=gs, validate=False, mode=mode,
+                                          plan=plan)
+                    tb.append(timed(bwd_j))
+                    if a.contention and Pr > 1:
+                        # the collective beside this part: forward -- the next part's all-gather
+                        # ((N-1)/N of world * vh * 5k bytes copied); backward -- the previous
+                        # part's reduce-scatter ((N-1)/N of world * vh * 4k, read twice)
+                        ag_b = world * vh * k * 5 * (world - 1) // world
+                        rs_b = world * vh * k * 4 * (world - 1) // world
+                        rec_fwd = a.records and mk.records_ok(sh.n_local, nc, cj.numel(), D, k)
+                        if rec_fwd:
+                            recj = mk.cbsr_records(cvj, cij, D)
+                            fwd_j = lambda: mk.spgemm_forward_records(  # noqa: E731
+                                rp, cj, vj, recj, k, D, out=y, accumulate=j > 0)
+                        else:
+                            fwd_j = lambda: mk.spgemm_forward(  # noqa: E731
+                                rp, cj, vj, cvj, cij, D, out=y, validate=False, accumulate=j > 0)
+                        for bw in a.busbw:
+                            cont.setdefault(bw, {"f": [], "b": [], "ag": [], "rs": []})
+                            f_ms, ag_ms = timed_beside(fwd_j, ag_b, False, bw)
+                            b_ms, rs_ms = timed_beside(bwd_j, rs_b, True, bw)
+                            cont[bw]["f"].append(f_ms)
+                            cont[bw]["b"].append(b_ms)
+                            cont[bw]["ag"].append(ag_ms)
+                            cont[bw]["rs"].append(rs_ms)
+                        if rec_fwd:
+                            del recj
                     del cvj, cij, gs, plan
                 ag, rs = world * vh * k * 5, world * vh * k * 4
                 if worst is None or sum(tf) + sum(tb) > sum(worst[0]) + sum(worst[1]):
-                    worst = (tf, tb, ag, rs, rank)
+                    worst = (tf, tb, ag, rs, rank, cont)
                 del sh, gl, y
-            tf, tb, ag, rs, rk = worst
+            tf, tb, ag, rs, rk, cont = worst
             print(f"  N={world} pipeline {Pn}: slowest rank {rk}: fwd parts "
                   f"{' + '.join(f'{x:.3f}' for x in tf)}, bwd parts "
                   f"{' + '.join(f'{x:.3f}' for x in tb)} ms; per part all-gather {ag / 1e6:.1f} MB, "
@@ -195,3 +290,18 @@ if a.pipelines:
                 t = step_model(tf, tb, ag, rs, world, bw)
                 sp = f", {base / t:.2f}x over N=1" if base else ""
                 print(f"     busbw {bw:.0f} GB/s: step {t:.3f} ms{sp}", flush=True)
+                if bw in cont:
+                    c = cont[bw]
+                    a_nom = ag * (world - 1) / world / (bw * 1e6)
+                    r_nom = rs * (world - 1) / world / (bw * 1e6)
+                    ac, rc = max(c["ag"]), max(c["rs"])
+                    tc = step_model_c(tf, c["f"], tb, c["b"], a_nom, max(a_nom, ac), r_nom,
+                                      max(r_nom, rc))
+                    spc = f", {base / tc:.2f}x over N=1" if base else ""
+                    print(f"       with contention ({a.channels} channels): fwd parts "
+                          f"{' + '.join(f'{x:.3f}' for x in c['f'])} (alone "
+                          f"{' + '.join(f'{x:.3f}' for x in tf)}), bwd parts "
+                          f"{' + '.join(f'{x:.3f}' for x in c['b'])} (alone "
+                          f"{' + '.join(f'{x:.3f}' for x in tb)}); stand-in all-gather "
+                          f"{ac:.3f} ms (nominal {a_nom:.3f}), reduce-scatter {rc:.3f} ms "
+                          f"(nominal {r_nom:.3f}); step {tc:.3f} ms{spc}", flush=True)
