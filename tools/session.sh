@@ -22,7 +22,7 @@
 #   topkab    top-k GPU tests, then tools/topk_ab.py alternating the product library and the
 #             variants in $VARS (lib/variants/<name>, tools/tune.sh), two repeats
 #   ab        tools/ab_bench.sh over the variants in $VARS and the bench argument strings in
-#             $ABCFGS (separated by ';'); $R repeats
+#             $ABCFGS (separated by ';'); $REPS repeats (2)
 #   window    the products forward with its columns folded into cache-sized windows
 #             (tools/fwd_slice_probe.py, k = 8 and 16)
 #   rehearse  N-rank rehearsals of the multi-GPU bench on the one GPU (gloo-staged
@@ -212,7 +212,8 @@ step_ab() {
   mkdir -p $O/ab
   local cfgs=()
   IFS=';' read -ra cfgs <<< "${ABCFGS:?ABCFGS=\"--k 16;--graph products --k 8\"}"
-  timeout -k 10 900 bash tools/ab_bench.sh "base ${VARS:?}" "${cfgs[@]}" > $O/ab/ab.txt 2>&1
+  R=${REPS:-2} timeout -k 10 900 bash tools/ab_bench.sh "base ${VARS:?}" "${cfgs[@]}" \
+    > $O/ab/ab.txt 2>&1
   cat $O/ab/ab.txt
 }
 step_window() {
