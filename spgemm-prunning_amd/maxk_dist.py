@@ -423,15 +423,20 @@ class ShardedMaxK:
         the gathered vertices); the part's selectors for the backward are its columns 4k..5k."""
         P, vh = self.pipeline, self.vh
         dev = sv.device
-        recvs, works = [], []
+        # every part's send buffer stays referenced until its all-gather has been waited on (the
+        # caching allocator also holds a block used on the communicator's stream, but the
+        # lifetime does not rest on that)
+        recvs, works, sends = [], [], []
         for j in range(P):
             send = self.kernels.cbsr_records(sv[j * vh:(j + 1) * vh], si[j * vh:(j + 1) * vh], D)
             rr = torch.empty(self.world * vh, 5 * k, dtype=torch.uint8, device=dev)
             works.append(all_gather_rows(rr.view(-1), send.view(-1), self.group, async_op=True))
             recvs.append(rr)
+            sends.append(send)
         y, saved = out, []
         for j in range(P):
             _wait(works[j])
+            sends[j] = None
             rr = recvs[j]
             rp, col, val = self.parts[j]
             saved.append((rr[:, 4 * k:].contiguous(), None))

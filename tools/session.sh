@@ -41,6 +41,14 @@
 #             with each part's kernels also timed beside a paced copy standing in for the
 #             overlapping RCCL collective (tools/paced_copy.hip, 32 and 64 channels): the
 #             contention-inclusive N = 8 step model (r06)
+#   phases    box identity and clocks (rocm-smi), then rocprofv3 --kernel-trace --stats of the
+#             ogbn-products k = 32 bench (csc phase 1 / phase 2 per-kernel times) and of the
+#             default Reddit bench: run on several boxes to name the phase behind the products
+#             backward's box-to-box spread (r06)
+#   spread    tools/clock_probe.py (products k = 32 forward + csc backward in a 12-s loop) under
+#             rocprofv3 --kernel-trace --stats, with rocm-smi clocks / power / temperature
+#             sampled from the shell every second beside it: per-phase times and the clocks
+#             they ran at, on whichever box this call got (r06)
 #   collect   (here, not on the box) copy gpurun_out/<round> into profiles/<round> and write
 #             the summaries (kernel stats, PMC traffic.json, presets and kernel-test tables)
 set -eo pipefail
@@ -188,6 +196,42 @@ step_contention() {
       > $O/scaling/contention_products_k32_ch$ch.txt 2>&1
     tail -12 $O/scaling/contention_products_k32_ch$ch.txt
   done
+}
+step_phases() {
+  local d=$O/phases/$(date +%H%M%S)
+  mkdir -p $d
+  { hostname; rocm-smi --showproductname --showclocks --showtemp --showpower 2>&1 || true; } \
+    > $d/smi_before.txt
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d/products_k32 -o run \
+    --output-format csv -- python3 bench.py --graph products --k 32 --steps 20 --warmup 5 \
+    --no-cpu-baseline --no-cpu-spmm --no-rocsparse > $d/products_k32.json 2> $d/products_k32.err
+  python tools/stats_summary.py $d/products_k32/run_kernel_stats.csv $d/products_k32.json \
+    > $d/products_k32.txt
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d/reddit -o run \
+    --output-format csv -- python3 bench.py --steps 20 --warmup 5 \
+    --no-cpu-baseline --no-cpu-spmm --no-rocsparse > $d/reddit.json 2> $d/reddit.err
+  python tools/stats_summary.py $d/reddit/run_kernel_stats.csv $d/reddit.json > $d/reddit.txt
+  { rocm-smi --showclocks --showtemp --showpower 2>&1 || true; } > $d/smi_after.txt
+  head -12 $d/products_k32.txt
+  grep -i 'sclk\|mclk\|fclk' $d/smi_before.txt | head -6 || true
+}
+step_spread() {
+  local d=$O/spread/$(date +%H%M%S)
+  mkdir -p $d
+  { rocm-smi --showproductname --showuniqueid 2>&1 || true; } > $d/box.txt
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $d/prof -o run --output-format csv \
+    -- python3 tools/clock_probe.py --seconds 12 > $d/probe.txt 2> $d/probe.err &
+  local pid=$! i
+  for i in $(seq 60); do
+    kill -0 $pid 2>/dev/null || break
+    { date +%s.%N; rocm-smi --showclocks --showpower --showtemp 2>&1 | grep -E 'sclk|mclk|fclk|Power|junction|memory' || true; } >> $d/clocks.txt
+    sleep 1
+  done
+  wait $pid
+  python tools/stats_summary.py $d/prof/run_kernel_stats.csv > $d/stats.txt
+  head -6 $d/stats.txt
+  grep -i guid\|unique $d/box.txt | head -2 || true
+  tail -3 $d/probe.txt
 }
 step_statscfg() {
   mkdir -p $O/stats_cfg
