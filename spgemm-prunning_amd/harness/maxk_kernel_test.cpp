@@ -19,6 +19,9 @@
 // pull locality) unless --bwd names one; its per-graph plan is built before the timing, the
 // analogue of the reference's .warp4 files.
 //
+// --graph-replay (r06): every timed MaxK call is captured once into a hipGraph and timed as one
+// hipGraphLaunch + synchronize (the library SpMM too, when its calls capture), so the wall
+// clock shows the kernels without the per-kernel launch cost of a multi-kernel op.
 // Extra modes for testing through the C ABI alone:
 //   --check            check_err (main.cu:19-48, disabled in the reference) of the forward
 //                      against the library SpMM: error sum, "validation pass!" below 1e-3 mean;
@@ -122,9 +125,49 @@ std::vector<T> download(const Buf &b, size_t count) {
     return v;
 }
 
+// The stream every timed call launches on: the legacy default stream, or with --graph-replay
+// a created one whose calls are captured into a hipGraph (r06).
+hipStream_t g_stream = nullptr;
+bool g_replay = false;
+
 // SPMM_BASE::timing_body (spmm_base.h:34-61): `times` warmup runs, then `times` timed runs,
-// each bracketed by a device synchronize; returns the mean in seconds
-double timing_body(const std::function<void()> &run, int times) {
+// each bracketed by a device synchronize; returns the mean in seconds.  --graph-replay: the
+// call is captured once on g_stream into a hipGraph and each run is one hipGraphLaunch of it
+// (the op's several kernels leave the host in one submission) -- the same wall clock around
+// it.  A call that cannot be captured (the library's) runs as is; `replayed` says which.
+double timing_body(const std::function<void()> &run, int times, bool *replayed = nullptr) {
+    if (replayed) *replayed = false;
+    if (g_replay) {
+        HIP_CHECK(hipDeviceSynchronize());  // setup on the legacy stream (plans) has finished
+        run();  // first call outside the capture (lazy one-time setup in the library)
+        HIP_CHECK(hipStreamSynchronize(g_stream));
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        bool ok = hipStreamBeginCapture(g_stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        if (ok) {
+            run();
+            ok = hipStreamEndCapture(g_stream, &graph) == hipSuccess && graph != nullptr &&
+                 hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
+        }
+        if (ok) {
+            for (int i = 0; i < times; ++i) HIP_CHECK(hipGraphLaunch(exec, g_stream));
+            HIP_CHECK(hipStreamSynchronize(g_stream));
+            double total = 0;
+            for (int i = 0; i < times; ++i) {
+                const auto t0 = std::chrono::system_clock::now();
+                HIP_CHECK(hipGraphLaunch(exec, g_stream));
+                HIP_CHECK(hipStreamSynchronize(g_stream));
+                const auto t1 = std::chrono::system_clock::now();
+                total += std::chrono::duration<double>(t1 - t0).count();
+            }
+            HIP_CHECK(hipGraphExecDestroy(exec));
+            HIP_CHECK(hipGraphDestroy(graph));
+            if (replayed) *replayed = true;
+            return total / times;
+        }
+        (void)hipGetLastError();
+        if (graph) (void)hipGraphDestroy(graph);
+    }
     for (int i = 0; i < times; ++i) run();
     HIP_CHECK(hipDeviceSynchronize());
     double total = 0;
@@ -207,7 +250,7 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
             b.run = [&b, G, row_div, S, out, V, E, D, k] {
                 MAXK_CHECK(maxk_sspmm_backward_pull(G, row_div, S, b.plan_a.as<int32_t>(),
                                                     b.plan_b.as<uint32_t>(), b.shift, b.slices,
-                                                    out, V, V, E, D, k, b.ws.p, b.ws.n, nullptr));
+                                                    out, V, V, E, D, k, b.ws.p, b.ws.n, g_stream));
             };
             return;
         }
@@ -253,7 +296,7 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
                     b.ent_pull.as<uint32_t>(), b.counts[1], b.shift, b.slices,
                     b.off_ip.as<int32_t>(), b.off_col.as<int32_t>(), b.off_val.as<float>(),
                     b.counts[2], b.off_cp.as<int32_t>(), b.off_eid.as<int32_t>(), 0, out, V, V, D,
-                    k, b.ws.p, b.ws.n, nullptr, nullptr, nullptr, nullptr));
+                    k, b.ws.p, b.ws.n, g_stream, nullptr, nullptr, nullptr));
             };
             return;
         }
@@ -276,7 +319,7 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
                 MAXK_CHECK(maxk_sspmm_backward_bsort(
                     rp, ci, ev, G, row_div, S, nullptr, b.plan_a.as<int32_t>(),
                     b.plan_b.as<int32_t>(), b.plan_c.as<uint16_t>(), b.plan_d.as<uint16_t>(),
-                    b.plan_e.as<int32_t>(), b.shift, out, V, V, E, D, k, b.ws.p, b.ws.n, nullptr));
+                    b.plan_e.as<int32_t>(), b.shift, out, V, V, E, D, k, b.ws.p, b.ws.n, g_stream));
             };
             return;
         }
@@ -297,7 +340,7 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
             b.run = [&b, G, row_div, S, out, V, E, D, k] {
                 MAXK_CHECK(maxk_sspmm_backward_dense(b.plan_a.as<int32_t>(), b.plan_c.as<int32_t>(),
                                                      b.plan_d.as<float>(), G, row_div, S, out, V,
-                                                     V, E, D, k, 0, b.ws.p, b.ws.n, nullptr));
+                                                     V, E, D, k, 0, b.ws.p, b.ws.n, g_stream));
             };
             return;
         }
@@ -305,7 +348,7 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
             b.ws.alloc(maxk_sspmm_backward_workspace_size(V, V, E, D, k, 0));
             b.run = [&b, rp, ci, ev, G, row_div, S, out, V, E, D, k] {
                 MAXK_CHECK(maxk_sspmm_backward(rp, ci, ev, G, row_div, S, out, V, V, E, D, k, 0,
-                                               b.ws.p, b.ws.n, nullptr));
+                                               b.ws.p, b.ws.n, g_stream));
             };
             return;
         }
@@ -320,7 +363,7 @@ void build_backward(Backward &b, const Buf &ip, const Buf &ix, const Buf &val, c
             b.run = [&b, rp, ci, ev, G, row_div, S, out, V, E, D, k] {
                 MAXK_CHECK(maxk_sspmm_backward_csc(rp, ci, ev, G, row_div, S, b.plan_a.as<int32_t>(),
                                                    b.plan_b.as<int32_t>(), out, V, V, E, D, k, 0,
-                                                   b.ws.p, b.ws.n, nullptr));
+                                                   b.ws.p, b.ws.n, g_stream));
             };
             return;
         }
@@ -440,10 +483,12 @@ int test_graph(const Options &o, const std::string &graph, int cur, int total) {
             MAXK_CHECK(maxk_dense_spmm_plan_create(&plan, ip.as<int32_t>(), ix.as<int32_t>(),
                                                    val.as<float>(), dense.as<float>(),
                                                    ylib.as<float>(), V, V, E, D, 0, nullptr));
-            const double t = timing_body([&] { MAXK_CHECK(maxk_dense_spmm_run(plan, nullptr)); },
-                                         o.lib_runs);
+            bool rep = false;
+            const double t = timing_body([&] { MAXK_CHECK(maxk_dense_spmm_run(plan, g_stream)); },
+                                         o.lib_runs, &rep);
             MAXK_CHECK(maxk_dense_spmm_plan_destroy(plan));
             if (n == 0) std::cout << tag << " cusparse " << t * 1000 << std::endl;
+            if (g_replay) std::cerr << "# " << tag << " library SpMM graph-replayed " << rep << std::endl;
         }
 
         const size_t fws_b = maxk_spgemm_forward_workspace_size(V, V, E, D, k, 0);
@@ -451,9 +496,10 @@ int test_graph(const Options &o, const std::string &graph, int cur, int total) {
         auto fwd = [&] {
             MAXK_CHECK(maxk_spgemm_forward(ip.as<int32_t>(), ix.as<int32_t>(), val.as<float>(),
                                            sv.as<float>(), ss.as<uint8_t>(), row_div, y.as<float>(),
-                                           V, V, E, D, k, 0, fws.p, fws.n, nullptr));
+                                           V, V, E, D, k, 0, fws.p, fws.n, g_stream));
         };
-        const double t_f = timing_body(fwd, o.runs);
+        bool rep_f = false, rep_b = false;
+        const double t_f = timing_body(fwd, o.runs, &rep_f);
         std::cout << tag << " maxk " << t_f * 1000 << std::endl;
         if (o.check) {
             bool has_err = false;
@@ -480,9 +526,12 @@ int test_graph(const Options &o, const std::string &graph, int cur, int total) {
             }
         }
         build_backward(b, ip, ix, val, G, rdiv, row_div, ss, gs, V, E, D, k);
-        const double t_b = timing_body(b.run, o.runs);
+        const double t_b = timing_body(b.run, o.runs, &rep_b);
         std::cout << tag << " maxk_backward " << t_b * 1000 << std::endl;
         std::cerr << "# " << tag << " backward mode " << mode_name(b.mode) << std::endl;
+        if (g_replay)
+            std::cerr << "# " << tag << " graph-replayed forward " << rep_f << " backward " << rep_b
+                      << std::endl;
         if (!o.dump.empty()) {
             write_array(o.dump + "/y.f32", download<float>(y, (size_t)V * D));
             write_array(o.dump + "/gs.f32", download<float>(gs, (size_t)V * k));
@@ -525,10 +574,11 @@ int main(int argc, char **argv) {
         else if (a == "--dump") o.dump = next();
         else if (a == "--runs") o.runs = std::atoi(next().c_str());
         else if (a == "--lib-runs") o.lib_runs = std::atoi(next().c_str());
+        else if (a == "--graph-replay") g_replay = true;
         else if (a == "-h" || a == "--help") {
             std::printf("usage: %s [graph] [--dir DIR] [--k 16,32,64] [--dim 256] "
-                        "[--bwd auto|pull|csc|hybrid|bucket|bsort|atomic|dense] [--check] [--runs 4] "
-                        "[--inputs DIR] [--dump DIR]\n", argv[0]);
+                        "[--bwd auto|pull|csc|hybrid|bsort|atomic|dense] [--check] [--runs 4] "
+                        "[--inputs DIR] [--dump DIR] [--graph-replay]\n", argv[0]);
             return 0;
         } else if (!a.empty() && a[0] != '-') o.graph = a;
         else {
@@ -537,13 +587,14 @@ int main(int argc, char **argv) {
         }
     }
     if (o.bwd != "auto" && mode_of(o.bwd) < 0) {
-        std::fprintf(stderr, "--bwd must be auto, pull, csc, hybrid, bucket, bsort or atomic\n");
+        std::fprintf(stderr, "--bwd must be auto, pull, csc, hybrid, bsort, atomic or dense\n");
         return 1;
     }
     if (maxk_device_count() < 1) {
         std::fprintf(stderr, "no HIP device\n");
         return 4;
     }
+    if (g_replay) HIP_CHECK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
     if (!o.graph.empty()) return test_graph(o, o.graph, 1, 1);
     // every <dir>/*.indptr (main.cu:197-217)
     std::vector<std::string> graphs;

@@ -49,6 +49,10 @@
 #             rocprofv3 --kernel-trace --stats, with rocm-smi clocks / power / temperature
 #             sampled from the shell every second beside it: per-phase times and the clocks
 #             they ran at, on whichever box this call got (r06)
+#   ktg       the compiled harness on the Flickr- and Reddit-sized graphs, plain and with
+#             --graph-replay (each op captured once into a hipGraph and timed as one launch),
+#             plus rocprofv3 --kernel-trace --stats of the plain Flickr run (the ops' kernel time
+#             beside their wall time: the launch-gap share; r06)
 #   collect   (here, not on the box) copy gpurun_out/<round> into profiles/<round> and write
 #             the summaries (kernel stats, PMC traffic.json, presets and kernel-test tables)
 set -eo pipefail
@@ -232,6 +236,29 @@ step_spread() {
   head -6 $d/stats.txt
   grep -i guid\|unique $d/box.txt | head -2 || true
   tail -3 $d/probe.txt
+}
+step_ktg() {
+  local d=$O/kernel_test_graph g D
+  mkdir -p $d
+  for g in flickr reddit; do
+    D=256; [ $g = flickr ] && D=64
+    timeout -k 10 300 python -c "
+import sys; sys.path.insert(0, 'spgemm-prunning_amd')
+import torch, maxk_graph
+rp, col = maxk_graph.synthetic_graph('$g', device=torch.device('cuda'))
+maxk_graph.save_graph(rp, col, '/tmp/maxk_graphs', '$g')"
+    timeout -k 10 300 spgemm-prunning_amd/bin/maxk_kernel_test $g --dir /tmp/maxk_graphs \
+      --dim $D --k 8,16,32,64 --runs 20 > $d/$g.txt 2> $d/$g.err
+    timeout -k 10 300 spgemm-prunning_amd/bin/maxk_kernel_test $g --dir /tmp/maxk_graphs \
+      --dim $D --k 8,16,32,64 --runs 20 --graph-replay > $d/${g}_replay.txt 2> $d/${g}_replay.err
+    if [ $g = flickr ]; then
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d/prof_flickr -o run \
+        --output-format csv -- spgemm-prunning_amd/bin/maxk_kernel_test $g \
+        --dir /tmp/maxk_graphs --dim $D --k 16 --runs 20 > $d/flickr_prof.txt 2>&1
+    fi
+    rm -f /tmp/maxk_graphs/$g.indptr /tmp/maxk_graphs/$g.indices
+  done
+  paste $d/flickr.txt $d/flickr_replay.txt | head -20
 }
 step_statscfg() {
   mkdir -p $O/stats_cfg
