@@ -144,6 +144,7 @@ def test_sharded_forced_backward_modes(graph, single, bwd, stream, monkeypatch):
 
 @pytest.mark.parametrize("graph,k,gpus,records", [("products", 32, 2, True),
                                                   ("products", 32, 4, True),
+                                                  ("products", 32, 8, True),
                                                   ("reddit", 16, 8, False)])
 def test_bench_self_launch(graph, k, gpus, records):
     """BASELINE.json configs[3] (and the driver's default-graph SCALE shape) at real size through
@@ -152,8 +153,9 @@ def test_bench_self_launch(graph, k, gpus, records):
     torch.distributed.run, gloo-staged collectives on this one GPU), shards the graph by vertex
     range and checks every rank's forward rows and CBSR-gradient rows against the unsharded HIP
     result, which tests/test_fullsize_gpu.py pins to the oracle on every row.  ogbn-products at
-    k = 32 (V = 2,449,029, E = 123.7M) takes the pipelined transport-record exchange at N = 2 and
-    4; Reddit at k = 16 and N = 8 (`bench.py --gpus 8`, the driver's default graph) one part.
+    k = 32 (V = 2,449,029, E = 123.7M) takes the pipelined transport-record exchange at N = 2, 4
+    and 8 (configs[3]'s shapes); Reddit at k = 16 and N = 8 (`bench.py --gpus 8`, the driver's
+    default graph) one part.
     World > 1 over RCCL itself stays unmeasured on this one-GPU box."""
     import json
     env = dict(os.environ)
