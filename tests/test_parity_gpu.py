@@ -84,6 +84,40 @@ def test_forward_dense_small_k(mk, cuda, k, D, chunk):
     assert torch.equal(es, T(ti, cuda)[T(col, cuda).long()])
 
 
+@pytest.mark.parametrize("k", [8, 16, 24, 32])
+@pytest.mark.parametrize("D,chunk", [(256, 0), (256, 97), (64, 0)])
+def test_forward_emit_sparse_repeats(mk, cuda, k, D, chunk):
+    """The stream-writing forward on a sparse graph with rows past the streaming walker's 64
+    edges, a hub row split over items and repeated selectors (which the records fold into
+    their first occurrence): its output matches the oracle and the plain call (the plain one
+    streams rows, over 5k-byte transport records at k = 24 / 32), and the stream holds the
+    caller's selector bytes, repeats included."""
+    rng = np.random.default_rng(2000 + k + D + chunk)
+    V = 3000
+    deg = np.minimum(rng.geometric(1 / 20, V), 300)
+    deg[11] = 2500  # a hub row, split over items at chunk 97
+    deg[12] = 0
+    rp = np.zeros(V + 1, np.int32)
+    rp[1:] = np.cumsum(deg)
+    E = int(rp[-1])
+    assert E < 128 * V  # sparse: the streaming forward
+    col = np.concatenate([np.sort(rng.choice(V, int(d), replace=False)) for d in deg]).astype(np.int32)
+    val = rng.random(E, dtype=np.float32)
+    x = rng.standard_normal((V, D)).astype(np.float32)
+    tv, ti = O.topk(x, k)
+    dup = rng.random(V) < 0.2
+    ti[dup, 1] = ti[dup, 0]  # repeated selectors
+    div = np.maximum(deg, 1).astype(np.float32)
+    ref = O.spgemm_fwd(rp, col, val, tv, ti, D, row_div=div)
+    args = (T(rp, cuda), T(col, cuda), T(val, cuda), T(tv, cuda), T(ti, cuda), D)
+    y = mk.spgemm_forward(*args, row_div=T(div, cuda), chunk=chunk)
+    close(y, ref)
+    es = torch.full((E, k), 0xAB, dtype=torch.uint8, device=cuda)
+    ye = mk.spgemm_forward(*args, row_div=T(div, cuda), chunk=chunk, edge_sel_out=es)
+    close(ye, ref)
+    assert torch.equal(es, T(ti, cuda)[T(col, cuda).long()])
+
+
 @pytest.mark.parametrize("chunk", [0, 5, 37, 300])
 @pytest.mark.parametrize("path", CASES, ids=IDS)
 def test_forward_golden(mk, cuda, path, chunk):
