@@ -62,7 +62,6 @@ OP_KERNELS = {
     # gprime_kernel when a row_div is given (the bench passes none)
     "sspmm_backward_pull": ["pull_q_kernel", "pull_reduce_kernel", "pull_sel4_kernel",
                             "pull_sel_kernel", "pull_tile_kernel", "gprime_kernel"],
-    "sspmm_backward_bucket": ["sspmm_bwd_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_bsort": ["bsort_push_kernel", "bucket_sum_kernel", "bucket_fixup_kernel"],
     "sspmm_backward_atomic": ["sspmm_bwd_kernel"],
     # dense rows with the selecting store (k >= D / 2), or selected columns per lane
@@ -667,18 +666,32 @@ def main():
     adj_err = abs(float(a) - float(b)) / max(1.0, abs(float(a)))
 
     if world > 1:
-        # every rank holds the whole graph and X/G (same seeds): recompute its rows unsharded
-        cv_f, ci_f = mk.topk_cbsr(X, k)
-        y_f = mk.spgemm_forward(row_ptr, col, val, cv_f, ci_f, D, validate=False)[v0:v1]
-        gs_f = mk.sspmm_backward(row_ptr, col, val, G, ci_f, validate=False,
-                                 mode=args.bwd_mode)[v0:v1]
-        errs = torch.tensor([
-            float(((y - y_f).abs() / y_f.abs().clamp(min=1)).max()) if nl else 0.0,
-            float(((gs_loc[:nl] - gs_f).abs() / gs_f.abs().clamp(min=1)).max()) if nl else 0.0],
-            dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        # every rank holds the whole graph and X/G (same seeds): recompute its rows unsharded.
+        # Ranks sharing a device (the gloo rehearsal) take turns: eight concurrent unsharded
+        # products-sized backwards (a 15.8 GB contribution array each) could exhaust the one
+        # GPU's memory; each rank frees its cached blocks after its turn.
+        shared = world > ndev
+        err_local = [0.0, 0.0]
+        for turn in range(world if shared else 1):
+            if not shared or turn == rank:
+                cv_f, ci_f = mk.topk_cbsr(X, k)
+                y_f = mk.spgemm_forward(row_ptr, col, val, cv_f, ci_f, D, validate=False)[v0:v1]
+                gs_f = mk.sspmm_backward(row_ptr, col, val, G, ci_f, validate=False,
+                                         mode=args.bwd_mode)[v0:v1]
+                err_local = [
+                    float(((y - y_f).abs() / y_f.abs().clamp(min=1)).max()) if nl else 0.0,
+                    float(((gs_loc[:nl] - gs_f).abs() / gs_f.abs().clamp(min=1)).max())
+                    if nl else 0.0]
+                del y_f, gs_f, cv_f, ci_f
+                if shared:
+                    torch.cuda.synchronize()
+                    torch.cuda.empty_cache()
+            if shared:
+                dist.barrier()
+        errs = torch.tensor(err_local, dtype=torch.float64,
+                            device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(errs, op=dist.ReduceOp.MAX)
         dist_err = [float(errs[0]), float(errs[1])]
-        del y_f, gs_f, cv_f, ci_f
         stage("unsharded self-check done")
 
     fwd_ms = [e[0].elapsed_time(e[1]) for e in evs]

@@ -194,6 +194,9 @@ constexpr size_t kInfinityCacheBytes = 256ull << 20;  // MI355X MALL (MI355X_MIC
 #ifndef MAXK_CSC_GROUP_U  // csc_groups: slots per lane-group step
 #define MAXK_CSC_GROUP_U 4
 #endif
+#ifndef MAXK_T_LOAD_NT  // csc phase 2: non-temporal reads of whole-line T rows (k % 32 == 0)
+#define MAXK_T_LOAD_NT 1
+#endif
 #ifndef MAXK_SUM_U  // phase-2 depth; 0 = chosen per launch from the average in-degree
 #define MAXK_SUM_U 0
 #endif

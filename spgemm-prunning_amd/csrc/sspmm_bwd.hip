@@ -36,6 +36,20 @@ namespace {
 enum { kAtomic = 0, kStore = 1, kStoreX4 = 2, kStoreX4W = 3, kStoreX4S = 4 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// A contribution row's 16 B in phase 2.  NT: rows of whole 128-B lines (k % 32 == 0) are read
+// once, so non-temporally -- ogbn-products-sized csc backward k = 32 7.85 -> 7.77 ms, with the
+// selector stream 6.71 -> 6.60, k = 64 15.14 -> 14.75; rows sharing a line (k <= 16) need
+// the line kept for the other row, and lose 3-6 % that way (Reddit-sized csc k = 16 3.86 ->
+// 4.10, products k = 16 5.17 -> 5.37, bsort k = 8 3.06 -> 3.15; profiles/r06/tune/t_load_nt/).
+template <bool NT>
+__device__ __forceinline__ float4 t_load4(const float4 *p) {
+    if constexpr (NT)
+        return __builtin_bit_cast(float4,
+                                  __builtin_nontemporal_load(reinterpret_cast<const f32x4 *>(p)));
+    return *p;
+}
 
 // kStoreX4 (k % 4 == 0): LR = pow2ceil(k/4) lanes per edge, each lane owning 4
 // consecutive l: one u32 selector load, four LDS reads, one 16-B store; 64/LR
@@ -335,7 +349,7 @@ __global__ __launch_bounds__(kBlock, MAXK_BWD_WAVES) void sspmm_bwd_kernel(
 // dst[0:k], in a fixed order.  VEC (k in {4,8,...,256}): LR = k/4 lanes per row
 // (16-B loads), 64/LR rows per wave step, U steps in flight; the row groups are
 // combined by xor butterflies.  Scalar: KG = pow2ceil(k) lanes per row.
-template <bool VEC, int KG, int U, typename EidAt>
+template <bool VEC, int KG, int U, bool NT = false, typename EidAt>
 __device__ __forceinline__ void segment_sum(const float *__restrict__ T, EidAt eid, int64_t tb,
                                             int64_t te, int k, float *__restrict__ dst, int lane) {
     if constexpr (VEC) {
@@ -349,7 +363,7 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T, EidAt e
             for (int u = 0; u < U; ++u) {
                 const int64_t t = base + u * RI + g;
                 const int e = eid(t < te ? t : tb);
-                v[u] = T4[(size_t)(uint32_t)e * LR + q];
+                v[u] = t_load4<NT>(&T4[(size_t)(uint32_t)e * LR + q]);
                 if (t >= te) v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
@@ -400,7 +414,7 @@ __device__ __forceinline__ void segment_sum(const float *__restrict__ T, EidAt e
 // gathers are issued before this step's sums.  Destinations are taken in order while owned by
 // the item (token < d1) and holding at most lmax of its slots; returns the first one not taken
 // (the caller sums a longer one with the whole wave).  k % 4 == 0.
-template <int U, typename EidAt>
+template <int U, bool NT = false, typename EidAt>
 __device__ __forceinline__ int csc_groups(const float *__restrict__ T, EidAt eid_at,
                                           const int32_t *__restrict__ col_ptr, int c,
                                           int num_cols, int64_t d1, int k, int lmax,
@@ -441,7 +455,7 @@ __device__ __forceinline__ int csc_groups(const float *__restrict__ T, EidAt eid
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (dst >= 0 && t + u < te) v[u] = T4[(size_t)(uint32_t)eid_at(t + u) * LR + q];
+            if (dst >= 0 && t + u < te) v[u] = t_load4<NT>(&T4[(size_t)(uint32_t)eid_at(t + u) * LR + q]);
         }
     };
     assign();
@@ -480,7 +494,7 @@ __device__ __forceinline__ int csc_groups(const float *__restrict__ T, EidAt eid
 constexpr int kCscStage = 2048;
 // GROUP (VEC, STAGED): destinations of at most kCscGroupMax slots go through csc_groups.
 constexpr int kCscGroupMax = 64;
-template <bool VEC, int KG, int U, bool STAGED, bool GROUP = false>
+template <bool VEC, int KG, int U, bool STAGED, bool GROUP = false, bool NT = false>
 __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restrict__ col_ptr,
                                                          const int32_t *__restrict__ eid,
                                                          const float *__restrict__ T,
@@ -520,14 +534,14 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
         int64_t se = (int64_t)col_ptr[c];
         if (d1 - c < se) se = d1 - c;
         if (sb < se) {
-            segment_sum<VEC, KG, U>(T, eid_at, sb, se, k, slab + (int64_t)item * k, lane);
+            segment_sum<VEC, KG, U, NT>(T, eid_at, sb, se, k, slab + (int64_t)item * k, lane);
             cont = c - 1;
         }
     }
     if (lane == 0) slab_row[item] = cont;
     for (; c < num_cols; ++c) {
         if constexpr (GROUP) {
-            c = csc_groups<U>(T, eid_at, col_ptr, c, num_cols, d1, k, kCscGroupMax, grad_cbsr,
+            c = csc_groups<U, NT>(T, eid_at, col_ptr, c, num_cols, d1, k, kCscGroupMax, grad_cbsr,
                               lane);
             if (c >= num_cols) break;
         }
@@ -535,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void csc_sum_kernel(const int32_t *__restri
         if (cb + c >= d1) break;
         int64_t se = (int64_t)col_ptr[c + 1];
         if (d1 - c - 1 < se) se = d1 - c - 1;
-        segment_sum<VEC, KG, U>(T, eid_at, cb, se, k, grad_cbsr + (int64_t)c * k, lane);
+        segment_sum<VEC, KG, U, NT>(T, eid_at, cb, se, k, grad_cbsr + (int64_t)c * k, lane);
     }
 }
 
@@ -1648,18 +1662,29 @@ int csc_impl(const int32_t *row_ptr, const int32_t *col_idx, const float *edge_v
     const int nc = (int)num_cols;
     const bool staged = MAXK_CSC_STAGE && L.chunk <= kCscStage;
     const size_t lds = (size_t)kWavesPerBlock * L.chunk * sizeof(int32_t);
+    // T rows of whole 128-B lines: non-temporal reads (t_load4)
+    const bool nt = MAXK_T_LOAD_NT && k % 32 == 0;
     if (staged && vec_sum(k) && k >= 16 && k <= 64 &&
         num_e < (int64_t)MAXK_CSC_GROUP_DEG * num_cols) {
         // few slots per destination: lane groups per destination (csc_groups)
-        hipLaunchKernelGGL((csc_sum_kernel<true, 64, MAXK_CSC_GROUP_U, true, true>), grid,
-                           dim3(kBlock), lds, s, col_ptr, csc_eid, T, grad_cbsr, slab, slab_row,
-                           nc, num_e, k, L.chunk, L.n_items);
+        if (nt)
+            hipLaunchKernelGGL((csc_sum_kernel<true, 64, MAXK_CSC_GROUP_U, true, true, true>),
+                               grid, dim3(kBlock), lds, s, col_ptr, csc_eid, T, grad_cbsr, slab,
+                               slab_row, nc, num_e, k, L.chunk, L.n_items);
+        else
+            hipLaunchKernelGGL((csc_sum_kernel<true, 64, MAXK_CSC_GROUP_U, true, true>), grid,
+                               dim3(kBlock), lds, s, col_ptr, csc_eid, T, grad_cbsr, slab,
+                               slab_row, nc, num_e, k, L.chunk, L.n_items);
     } else if (vec_sum(k)) {
         const int rows_per_step = kWave / (k / 4);
         const int u = MAXK_SUM_U > 0 ? MAXK_SUM_U
                                      : pick_depth(num_e, num_cols, rows_per_step, 2, 8);
 #define MAXK_SUM_LAUNCH(UV)                                                                  \
-    if (staged)                                                                              \
+    if (staged && nt)                                                                        \
+        hipLaunchKernelGGL((csc_sum_kernel<true, 64, UV, true, false, true>), grid,          \
+                           dim3(kBlock), lds, s, col_ptr, csc_eid, T, grad_cbsr, slab,       \
+                           slab_row, nc, num_e, k, L.chunk, L.n_items);                      \
+    else if (staged)                                                                         \
         hipLaunchKernelGGL((csc_sum_kernel<true, 64, UV, true>), grid, dim3(kBlock), lds, s, \
                            col_ptr, csc_eid, T, grad_cbsr, slab, slab_row, nc, num_e, k,     \
                            L.chunk, L.n_items);                                              \

@@ -166,7 +166,12 @@ def test_bench_self_launch(graph, k, gpus, records):
     p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", str(gpus),
                         "--graph", graph, "--k", str(k), "--steps", "2", "--warmup", "1"],
                        env=env, cwd=root, capture_output=True, text=True, timeout=280)
-    assert p.returncode == 0, p.stderr[-3000:]
+    if p.returncode != 0:
+        # a failing rank's own traceback sits above torch.distributed.run's summary
+        lines = p.stderr.splitlines()
+        hits = [i for i, ln in enumerate(lines) if "Traceback" in ln or "Error" in ln]
+        first = "\n".join(lines[max(0, hits[0] - 2):hits[0] + 40]) if hits else ""
+        raise AssertionError(f"rc {p.returncode}\n{first}\n...\n{p.stderr[-1500:]}")
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
     d = json.loads(lines[0])
