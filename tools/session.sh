@@ -12,7 +12,8 @@
 #   stats     rocprofv3 --kernel-trace --stats of a short default bench
 #   pmc       FETCH_SIZE and WRITE_SIZE of the same short bench, one rocprofv3 --pmc pass each
 #   presets   every preset with its denominators (rocSPARSE every algorithm; CPU baselines
-#             with PRESET_CPU=1); presets_small: the Flickr-shaped ones alone
+#             with PRESET_CPU=1); presets_small: the Flickr-shaped ones alone; presets_products:
+#             ogbn-products-sized k = 32 and 64 alone
 #   pmccfg    PMC passes of the non-default configurations in $CFGS
 #             ("name:--bench --args name2:..."), keyed by each run's traffic_key
 #   pmcset    counter sets $SETS ("C1 C2;C3 C4", one pass per set) over the configurations in
@@ -117,6 +118,11 @@ step_presets() {
   preset proteins --graph proteins
   step_presets_small
   preset products_comm_ordered --graph products_comm --reorder
+}
+# the ogbn-products-sized presets whose csc phase 2 reads whole-line rows (k % 32 == 0)
+step_presets_products() {
+  mkdir -p $O/presets
+  for k in 32 64; do preset products_k$k --graph products --k $k; done
 }
 # the Flickr-shaped graph (configs[0], D = 64) at every k: k >= 32 takes the dense route
 step_presets_small() {
