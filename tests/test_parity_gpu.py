@@ -929,6 +929,56 @@ def test_forward_stream_wide_records(mk, cuda, D, k):
         close(fwd(cv, cid, chunk=chunk), yd)
 
 
+@pytest.mark.parametrize("k", [8, 32])
+def test_tables_past_2_24_columns(mk, cuda, k):
+    """Maximum sizes of the column space: num_cols = 2^24 + 4099 source vertices, so record
+    offsets no longer fit the 24-bit multiply (the forward's 64-bit-address walker, WIDE; at
+    k = 32 the record table also passes 4 GiB) and phase 1 of the two-phase backward takes its
+    32-bit selector multiply (kStoreX4W).  A 1,500-row graph whose edges reach every part of
+    that range, including the last columns and a hub row split over items at chunk 50; the
+    forward and the csc / atomic / bsort / pull backwards against the oracle over the columns
+    the edges read (compacted), and every other gradient row exactly zero."""
+    rng = np.random.default_rng(77 + k)
+    NC = (1 << 24) + 4099
+    V, D = 1500, 256
+    deg = rng.integers(0, 40, V)
+    deg[5] = 900
+    rows = [np.sort(rng.choice(NC, int(d), replace=False)) for d in deg]
+    rows[9] = np.sort(np.concatenate([rows[9], NC - 1 - np.arange(3)]))  # the table's end
+    rp = np.zeros(V + 1, np.int64)
+    np.cumsum([len(r) for r in rows], out=rp[1:])
+    rp = rp.astype(np.int32)
+    col = np.concatenate(rows).astype(np.int32)
+    assert int(col.max()) == NC - 1 and (col >= (1 << 24)).sum() > 0
+    val = rng.random(col.size, dtype=np.float32)
+    uc = np.unique(col)
+    colc = np.searchsorted(uc, col).astype(np.int32)
+    cvc = rng.standard_normal((uc.size, k)).astype(np.float32)
+    cic = np.stack([rng.choice(D, k, replace=False) for _ in range(uc.size)]).astype(np.uint8)
+    div = np.maximum(np.diff(rp), 1).astype(np.float32)
+    G = rng.standard_normal((V, D)).astype(np.float32)
+    ucg = torch.from_numpy(uc.astype(np.int64)).to(cuda)
+    cv = torch.zeros(NC, k, device=cuda)
+    cv[ucg] = T(cvc, cuda)
+    ci = torch.arange(k, device=cuda, dtype=torch.uint8).repeat(NC, 1)
+    ci[ucg] = T(cic, cuda)
+    args = (T(rp, cuda), T(col, cuda), T(val, cuda))
+    yo = O.spgemm_fwd(rp, colc, val, cvc, cic, D, row_div=div)
+    go = O.sspmm_bwd(rp, colc, val, G, cic, row_div=div)
+    for chunk in (0, 50):
+        close(mk.spgemm_forward(*args, cv, ci, D, row_div=T(div, cuda), chunk=chunk), yo)
+    modes = ["csc", "atomic", "pull"] + (["bsort"] if k <= 8 else [])
+    for mode in modes:
+        for chunk in ((0, 50) if mode != "pull" else (0,)):
+            gs = mk.sspmm_backward(*args, T(G, cuda), ci, row_div=T(div, cuda), chunk=chunk,
+                                   mode=mode)
+            close(gs[ucg], go)
+            gs[ucg] = 0.0
+            assert not gs.any(), f"{mode}: rows no edge reads are not zero"
+            del gs
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("k", [4, 12, 16, 32])
 def test_forward_pack_aligned_and_not(mk, cuda, k):
     """The forward's record pack runs four l per thread (cbsr_pack4_kernel) on aligned CBSR
